@@ -1,0 +1,223 @@
+#!/usr/bin/env python
+"""Benchmark: the batched brute-force DM sweep (BASELINE.json configs[1]).
+
+Workload (one "step" = one sweep of one resident block):
+    C = 1024 channels x N = 2^20 samples x D = 1024 DM trials (0-1000 pc/cc,
+    uniform), 64 us sampling, 1250-1550 MHz band, float32 input (default) or
+    8-bit (--dtype u8), trim=True (plane width N - max delay = 1,034,083).
+Metric: DM-trial samples*channels per second (whole job), = D * n_out * C
+per step per rank / time.
+
+Multi-GPU (torchrun, one rank per GPU): time-block sharding -- every rank
+sweeps its OWN block (seeded by rank) over the full DM grid, no data-path
+collective ("scaling": "weak"); --mode dmshard instead broadcasts ONE block
+over RCCL and gives each rank a DM slice (pypulsar_amd.sharding).
+
+Timing: W untimed warm-up steps, then exactly K steps bracketed by a barrier
++ torch.cuda.synchronize(); the max over ranks is reported.  The sweep
+kernel's own duration is measured with HIP events on the stream it is
+launched on (torch's current stream) around every timed launch.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# MI355X peaks (MI355X_MICROARCH.md §Chip-level parameters)
+PEAK_HBM_GBS = 8000.0
+PEAK_F32_TFLOPS = 157.3   # FP32 vector peak == FP32 dense MFMA peak on gfx950
+
+CONFIGS = {
+    # BASELINE.json configs[1]
+    "config2": dict(C=1024, N=1 << 20, D=1024, dm_lo=0.0, dm_hi=1000.0),
+    # north-star single-GPU target (4096 ch x 2048 DM x 2^22)
+    "northstar": dict(C=4096, N=1 << 22, D=2048, dm_lo=0.0, dm_hi=1000.0),
+    "small": dict(C=256, N=1 << 18, D=256, dm_lo=0.0, dm_hi=500.0),
+}
+
+
+def band(C, lo=1250.0, hi=1550.0):
+    foff = -(hi - lo) / C
+    return (hi + foff / 2.0) + foff * np.arange(C)
+
+
+def synth_block(C, N, seed, dtype, device):
+    """uint8 clip(round(N(128, 16))) filterbank block, generated on the device."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    x = torch.empty((C, N), dtype=torch.float32, device=device)
+    x.normal_(128.0, 16.0, generator=g)
+    x = x.round_().clamp_(0, 255)
+    return x.to(torch.uint8) if dtype == "u8" else x
+
+
+def cpu_baseline(cfg, ntrials, dt):
+    """Oracle (NumPy restatement of Spectra.dedisperse + channel sum, C-order,
+    one core) on a bounded sample: ntrials full-length DM trials."""
+    from oracle import spectra_oracle as orc
+    C, N = cfg["C"], cfg["N"]
+    freqs = band(C)
+    rng = np.random.default_rng(0)
+    x = np.clip(np.round(rng.normal(128, 16, (C, N))), 0, 255).astype(np.float64)
+    dms = np.linspace(cfg["dm_lo"], cfg["dm_hi"], cfg["D"])
+    pick = dms[np.linspace(0, len(dms) - 1, ntrials).astype(int)]
+    work = 0
+    t0 = time.perf_counter()
+    for dm in pick:
+        d, _ = orc.dedisperse(x, freqs, dt, dm, padval=0, trim=True)
+        s = orc.channel_sum(d)
+        work += s.shape[0] * C
+    el = time.perf_counter() - t0
+    return dict(value=work / el, unit="samples*channels*DM/s", cores=1, kind="port",
+                sample="%d full-length DM trials (dedisperse(trim=True)+channel sum), "
+                       "%d ch x %d samples, float64 NumPy, 1 thread, %.1f s"
+                       % (ntrials, C, N, el))
+
+
+def load_pmc(path, key):
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(key)
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="config2", choices=sorted(CONFIGS))
+    ap.add_argument("--dtype", default="f32", choices=["f32", "u8"])
+    ap.add_argument("--mode", default="timeblock", choices=["timeblock", "dmshard"])
+    ap.add_argument("--cpu-trials", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import __graft_entry__ as g
+    if rank == 0:
+        g.build()
+    if world > 1:
+        dist.barrier()
+    g.build()
+    from pypulsar_amd.sweep import DMSweep
+
+    cfg = CONFIGS[args.config]
+    C, N, D = cfg["C"], cfg["N"], cfg["D"]
+    dt = 64e-6
+    freqs = band(C)
+    dms_all = np.linspace(cfg["dm_lo"], cfg["dm_hi"], D)
+
+    if args.mode == "timeblock":
+        dms = dms_all
+        x = synth_block(C, N, 1000 + rank, args.dtype, dev)
+    else:
+        from pypulsar_amd.sharding import dm_slices
+        lo, hi = dm_slices(D, world)[rank]
+        dms = dms_all[lo:hi]
+        x = synth_block(C, N, 1000, args.dtype, dev)
+    sw = DMSweep(dms, freqs, dt, dtype=args.dtype)
+    # plane width of the full grid (trim=True): identical on every rank
+    full_max = int(DMSweep(dms_all[-1:], freqs, dt).max_bin)
+    n_out = N - max(0, full_max)
+    plane = torch.empty((len(dms), n_out), dtype=torch.float32, device=dev)
+
+    def step():
+        return sw(x, out=plane)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        step()
+        evs[i][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    units_rank = len(dms) * n_out * C           # samples*channels*DM per step on this rank
+    units_all = (D * n_out * C) * (world if args.mode == "timeblock" else 1)
+    value = units_all * args.steps / el
+    s_in = 1 if args.dtype == "u8" else 4
+    adds_per_launch = units_rank                 # one FP32 add per work unit
+    achieved_tf = adds_per_launch / (kern_ms * 1e-3) / 1e12
+    uniq_bytes = C * N * s_in + len(dms) * n_out * 4
+    achieved_gbs = uniq_bytes / (kern_ms * 1e-3) / 1e9
+    pmc_key = "%s_%s" % (args.config, args.dtype)
+    traffic = load_pmc(os.path.join(ROOT, "profiles", "pmc_sweep.json"), pmc_key)
+
+    if rank == 0:
+        line = {
+            "metric": "DM-trial samples*channels/sec (node) + % HBM roofline",
+            "value": value,
+            "unit": "samples*channels*DM/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak" if args.mode == "timeblock" else "strong",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (uint8 clip(round(N(128,16))) filterbank%s, generated on device)"
+                    % ("" if args.dtype == "u8" else " as float32"),
+            "config": {"workload": "brute-force DM sweep %d ch x 2^%d samples x %d DM (%g-%g pc/cc), "
+                                   "64 us, 1250-1550 MHz, trim=True" % (C, int(np.log2(N)), D,
+                                                                      cfg["dm_lo"], cfg["dm_hi"]),
+                       "config_name": args.config, "channels": C, "samples": N, "dm_trials": D,
+                       "n_out": n_out, "parallelism": "%s%d" % ("tb" if args.mode == "timeblock"
+                                                                else "dm", world),
+                       "plan": sw.info(1 if args.dtype == "u8" else 0)},
+            "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_F32_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved_tf / PEAK_F32_TFLOPS,
+                         "traffic": traffic,
+                         "kernel": "pdd::k_sweep", "kernel_ms": kern_ms,
+                         "note": "compute roof: one FP32 add per samp*ch*DM; no MFMA-shaped "
+                                 "work exists, the FP32 vector peak equals the FP32 dense MFMA "
+                                 "peak (157.3 TF) on gfx950; see DESIGN.md"},
+            "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": PEAK_HBM_GBS,
+                             "unit": "GB/s", "frac": achieved_gbs / PEAK_HBM_GBS,
+                             "bytes_per_launch": uniq_bytes},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_trials, dt)
+        print(json.dumps(line))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

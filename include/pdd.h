@@ -1,0 +1,121 @@
+/*
+ * pdd.h — C ABI of libpdd.so, the MI355X (gfx950) incoherent-dedispersion
+ * engine behind pypulsar's `Spectra` hot path.
+ *
+ * Conventions:
+ *   - every entry point returns int status: 0 = ok, < 0 = error;
+ *     pdd_last_error() returns a thread-local message for the last failure;
+ *   - all array pointers are DEVICE pointers owned by the caller (torch
+ *     tensors or any hipMalloc'd memory) unless the name says `host_`;
+ *     the library never frees caller memory;
+ *   - every compute call takes a hipStream_t (passed as void*) and is
+ *     asynchronous on it; pdd_sync() is the only synchronisation;
+ *   - 2-D arrays are row-major with an explicit leading dimension `ld`
+ *     (elements between consecutive rows);
+ *   - the delay-bin tables are built on the host in float64 (bit-exact with
+ *     the reference) and passed in as int32.
+ *
+ * Each entry point cites the reference interface it replaces (file:line in
+ * emilieparent/pypulsar).
+ */
+#ifndef PDD_H
+#define PDD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* element types */
+enum { PDD_F32 = 0, PDD_U8 = 1, PDD_U16 = 2 };
+/* pad modes (Spectra.shift_channels padval, formats/spectra.py:81-94) */
+enum {
+  PDD_PAD_VALUE = 0,  /* per-channel pad value from `padvals` (number / 'mean' / 'median') */
+  PDD_PAD_ROTATE = 1  /* psr_utils.rotate wrap-around (padval == 'rotate') */
+};
+/* channel statistics (pad values for 'mean'/'median', spectra.py:83-86) */
+enum { PDD_STAT_MEAN = 0, PDD_STAT_MEDIAN = 1 };
+/* zero-DM layouts */
+enum { PDD_LAYOUT_TIME_MAJOR = 0, /* [nspec][nchan], filterbank file order */
+       PDD_LAYOUT_CHAN_MAJOR = 1  /* [nchan][nspec], Spectra.data order    */ };
+
+int pdd_version(void);
+const char* pdd_last_error(void);
+/* hipStreamSynchronize(stream) */
+int pdd_sync(void* stream);
+
+/* Corner turn [nspec][nchan] (in_dtype) -> [nchan][nspec] (out_dtype: PDD_F32,
+ * or the input dtype for a raw byte transpose).
+ * Replaces filterbank.get_spectra's reshape + `.T` + Spectra.__init__'s
+ * astype('float') (formats/filterbank.py:153-157, formats/spectra.py:34) and
+ * mockspecfil2subbands' per-block transpose (bin/mockspecfil2subbands.py:155-175). */
+int pdd_corner_turn(const void* in, int in_dtype, int64_t nspec, int64_t nchan, int64_t ld_in,
+                    void* out, int out_dtype, int64_t ld_out, void* stream);
+
+/* Elementwise dtype conversion of a [rows][cols] array to float32
+ * (Spectra.__init__ data.astype, formats/spectra.py:34, for C-ordered input). */
+int pdd_convert_f32(const void* in, int in_dtype, int64_t rows, int64_t cols, int64_t ld_in,
+                    float* out, int64_t ld_out, void* stream);
+
+/* Per-channel mean or median of x[C][N] -> out[C] (float32).
+ * Pad values of Spectra.shift_channels 'mean'/'median' (formats/spectra.py:83-86). */
+int pdd_channel_stats(const float* x, int64_t C, int64_t N, int64_t ld, int stat,
+                      float* out, void* stream);
+
+/* out[c][t] = X(c, t + bins[c]) for t < n_out, X = x inside [0,N), padvals[c]
+ * (PDD_PAD_VALUE) or wrap (PDD_PAD_ROTATE) outside.
+ * Replaces Spectra.shift_channels (formats/spectra.py:54-94) incl.
+ * psr_utils.rotate (spectra.py:80). `out` must not alias `x`. */
+int pdd_shift_pad(const float* x, int64_t C, int64_t N, int64_t ld, const int32_t* bins,
+                  int pad_mode, const float* padvals, float* out, int64_t ld_out,
+                  int64_t n_out, void* stream);
+
+/* Fused shift + group sum: out[k][t] = sum_{c in group k} X(c, t + bins[c]),
+ * groups = nsub contiguous blocks of C/nsub channels, t < n_out.
+ * nsub == nchan-groups: Spectra.subband (formats/spectra.py:96-138);
+ * nsub == 1: Spectra.dedisperse + channel sum, the dedispersed series of
+ * bin/waterfaller.py:140 (spectra.py:229-260).  bins may be NULL (no shift). */
+int pdd_shift_group_sum(const float* x, int64_t C, int64_t N, int64_t ld, const int32_t* bins,
+                        int pad_mode, const float* padvals, int64_t nsub, float* out,
+                        int64_t ld_out, int64_t n_out, void* stream);
+
+/* out[c][j] = sum_{k<factor} x[c][j*factor + k], j < N/factor.
+ * Replaces Spectra.downsample (formats/spectra.py:329-351). */
+int pdd_downsample(const float* x, int64_t C, int64_t N, int64_t ld, int64_t factor,
+                   float* out, int64_t ld_out, void* stream);
+
+/* Zero-DM filter: every spectrum minus its channel mean; integer data use
+ * round-half-even of the float64 mean and wrap modulo 2^nbits, float32 data
+ * stay float32.  Replaces bin/zero_dm_filter.py:30-50 (filter + write loop).
+ * `out` may alias `in`. */
+int pdd_zero_dm(const void* in, int dtype, int64_t nspec, int64_t nchan, int64_t ld,
+                int layout, void* out, int64_t ld_out, void* stream);
+
+/* ---- batched DM sweep (new executor over utils/DDplan2b.py grids) ----
+ * plane[d][t] = sum_c X(c, t + table[d][c]), t < n_out (defaults of
+ * Spectra.dedisperse(dm, padval, trim=True) + channel sum, per DM trial,
+ * formats/spectra.py:229-260 + bin/waterfaller.py:140).
+ * The plan holds the device copy of the delay table and its per-block
+ * extents; it is built once per (grid, channel count, dtype). */
+typedef struct pdd_sweep_plan pdd_sweep_plan;
+
+/* host_table: [D][C] int32, row d = the bins Spectra.dedisperse(dms[d])
+ * would pass to shift_channels.  dtype: PDD_F32 or PDD_U8 input. */
+int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int dtype,
+                          pdd_sweep_plan** plan);
+/* x: [C][N] (ld) of the plan's dtype; out: [D][ld_out] float32.
+ * For PDD_U8 with PDD_PAD_VALUE every padvals[c] must be an integer in
+ * [0, 255] (checked on the host side by the caller). */
+int pdd_sweep_execute(const pdd_sweep_plan* plan, const void* x, int64_t N, int64_t ld,
+                      int pad_mode, const float* padvals, float* out, int64_t ld_out,
+                      int64_t n_out, void* stream);
+/* Extents used by the plan (for DESIGN/bench reporting): DM trials, channels,
+ * DMs per block, time samples per block, LDS bytes per workgroup. */
+int pdd_sweep_plan_info(const pdd_sweep_plan* plan, int64_t* info /*[8]*/);
+int pdd_sweep_plan_destroy(pdd_sweep_plan* plan);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PDD_H */

@@ -1,0 +1,214 @@
+"""ORACLE (test infrastructure only; see oracle/__init__.py).
+
+NumPy restatement of the reference's Spectra hot path, float64 like the
+reference.  Each function cites the reference lines it follows.  Functions take
+and return plain arrays (no class state) so tests can compose them exactly the
+way the reference methods compose.
+"""
+import numpy as np
+
+# --------------------------------------------------------------------------
+# PRESTO psr_utils (not in the reference tree; restated; parity unpinned)
+# call sites: formats/spectra.py:80,126-127,247-248; utils/DDplan2b.py:129..382
+# --------------------------------------------------------------------------
+
+
+def delay_from_DM(dm, freqs):
+    """PRESTO psr_utils.delay_from_DM: DM / (0.000241 * f * f), 0 where f<=0.
+
+    Evaluated left to right, (0.000241*f)*f, in float64."""
+    f = np.asarray(freqs, dtype=np.float64)
+    with np.errstate(divide="ignore"):
+        return np.where(f > 0.0, dm / (0.000241 * f * f), 0.0)
+
+
+def rotate(arr, bins):
+    """PRESTO psr_utils.rotate: left rotation by ``bins mod len``."""
+    n = len(arr)
+    b = int(bins) % n
+    if b == 0:
+        return arr
+    return np.concatenate((arr[b:], arr[:b]))
+
+
+def dm_smear(dm, bw, fctr):
+    """PRESTO psr_utils.dm_smear: DM*BW/(0.0001205*f*f*f) seconds."""
+    return dm * bw / (0.0001205 * fctr * fctr * fctr)
+
+
+# --------------------------------------------------------------------------
+# formats/spectra.py
+# --------------------------------------------------------------------------
+
+
+def dedisperse_bins(dm, cur_dm, freqs, dt):
+    """Delay-bin table of Spectra.dedisperse, spectra.py:247-250."""
+    freqs = np.asarray(freqs, dtype=np.float64)
+    ref = delay_from_DM(dm - cur_dm, np.max(freqs))
+    rel = delay_from_DM(dm - cur_dm, freqs) - ref
+    return np.round(rel / dt).astype(np.int64)
+
+
+def subband_bins(subdm, cur_dm, freqs, dt, nsub):
+    """Delay-bin table of Spectra.subband, spectra.py:119-130 (py2 '/')."""
+    freqs = np.asarray(freqs, dtype=np.float64)
+    cps = len(freqs) // nsub
+    hi = freqs[np.arange(nsub) * cps]
+    ref = delay_from_DM(subdm - cur_dm, hi)
+    rel = delay_from_DM(subdm - cur_dm, freqs) - ref.repeat(cps)
+    return np.round(rel / dt).astype(np.int64)
+
+
+def subband_freqs(freqs, nsub):
+    """Subband centre frequencies, spectra.py:119-122,137."""
+    cps = len(freqs) // nsub
+    hi = freqs[np.arange(nsub) * cps]
+    lo = freqs[(1 + np.arange(nsub)) * cps - 1]
+    return 0.5 * (hi + lo)
+
+
+def shift_channels(data, bins, padval=0):
+    """Spectra.shift_channels, spectra.py:54-94 (per-channel loop, in place
+    on a copy).  Pad value for 'mean'/'median' is computed on the rotated
+    channel, before padding (spectra.py:80-86)."""
+    out = np.array(data, dtype=np.float64, copy=True)
+    assert out.shape[0] == len(bins)
+    for ii in range(out.shape[0]):
+        chan = out[ii]
+        b = int(bins[ii])
+        chan[:] = rotate(chan, b)
+        if isinstance(padval, str) and padval == "rotate":
+            continue
+        if isinstance(padval, str) and padval == "mean":
+            pad = np.mean(chan)
+        elif isinstance(padval, str) and padval == "median":
+            pad = np.median(chan)
+        else:
+            pad = padval
+        if b > 0:
+            chan[-b:] = pad
+        elif b < 0:
+            chan[:-b] = pad
+    return out
+
+
+def dedisperse(data, freqs, dt, dm, cur_dm=0.0, padval=0, trim=False):
+    """Spectra.dedisperse, spectra.py:229-260.  Returns (data, new_dm)."""
+    assert dm >= 0
+    bins = dedisperse_bins(dm, cur_dm, freqs, dt)
+    out = shift_channels(data, bins, padval)
+    if trim:
+        ntrim = max(bins)
+        if ntrim > 0:
+            out = out[:, :-ntrim]
+    return out, dm
+
+
+def subband(data, freqs, dt, nsub, subdm=None, cur_dm=0.0, padval=0):
+    """Spectra.subband, spectra.py:96-138.  Returns (data, new_freqs);
+    the Spectra's dm is NOT changed by subband."""
+    C = data.shape[0]
+    assert C % nsub == 0
+    assert subdm is None or subdm >= 0
+    out = np.asarray(data, dtype=np.float64)
+    if subdm is not None:
+        out = shift_channels(out, subband_bins(subdm, cur_dm, freqs, dt, nsub), padval)
+    out = np.array([np.sum(s, axis=0) for s in np.vsplit(out, nsub)])
+    return out, subband_freqs(np.asarray(freqs, dtype=np.float64), nsub)
+
+
+def trim(data, nbins, starttime, dt):
+    """Spectra.trim, spectra.py:305-327.  Returns (data, numspectra,
+    starttime); keeps the reference's bins<0 numspectra arithmetic."""
+    n = data.shape[1]
+    assert nbins < n
+    if nbins == 0:
+        return data, n, starttime
+    if nbins > 0:
+        return data[:, :-nbins], n - nbins, starttime
+    return data[:, nbins:], n - nbins, starttime + nbins * dt
+
+
+def downsample(data, dt, factor=1, trim_=True):
+    """Spectra.downsample, spectra.py:329-351 (py2 '/').  Returns (data, dt)."""
+    n = data.shape[1]
+    assert trim_ or not (n % factor)
+    new_n = n // factor
+    rem = n % factor
+    if rem:
+        data = data[:, :-rem]
+    out = data.reshape(data.shape[0], new_n, factor).sum(axis=2)
+    return out, dt * factor
+
+
+def channel_sum(data):
+    """Dedispersed series, bin/waterfaller.py:140 (data.data.sum(axis=0))."""
+    return np.asarray(data, dtype=np.float64).sum(axis=0)
+
+
+# --------------------------------------------------------------------------
+# bin/zero_dm_filter.py:30-39
+# --------------------------------------------------------------------------
+
+
+def zero_dm_filter(spectrum):
+    """One spectrum (all channels at one time sample): subtract the mean,
+    rounded half-even and cast to the data dtype when that differs (integer
+    data wraps modulo 2**nbits)."""
+    avg = spectrum.mean()
+    if avg.dtype != spectrum.dtype:
+        avg = np.round(avg).astype(spectrum.dtype)
+    return spectrum - avg
+
+
+def zero_dm_block(block):
+    """zero_dm_filter applied to every spectrum of a [nspec, nchan] block
+    (bin/zero_dm_filter.py:42-50 loop)."""
+    return np.array([zero_dm_filter(row) for row in block])
+
+
+# --------------------------------------------------------------------------
+# batched sweep (new; spec = per-DM dedisperse(trim) + channel sum)
+# --------------------------------------------------------------------------
+
+
+def sweep_table(dms, freqs, dt, cur_dm=0.0):
+    """[D, C] int64 table: row d = dedisperse_bins(dms[d])."""
+    return np.array([dedisperse_bins(dm, cur_dm, freqs, dt) for dm in dms], dtype=np.int64)
+
+
+def shifted_sum(data, bins, padval=0):
+    """Vectorised a4+a6: sum_c shift_channels(data, bins, padval)[c] (fast
+    restatement used for larger test sizes; equals channel_sum(shift_channels))."""
+    data = np.asarray(data, dtype=np.float64)
+    C, N = data.shape
+    t = np.arange(N)
+    acc = np.zeros(N, dtype=np.float64)
+    for c in range(C):
+        b = int(bins[c])
+        if isinstance(padval, str) and padval == "rotate":
+            acc += data[c, (t + b) % N]
+            continue
+        if isinstance(padval, str) and padval == "mean":
+            pad = np.mean(data[c])
+        elif isinstance(padval, str) and padval == "median":
+            pad = np.median(data[c])
+        else:
+            pad = float(padval)
+        s = t + b
+        ok = (s >= 0) & (s < N)
+        row = np.full(N, pad)
+        row[ok] = data[c, s[ok]]
+        acc += row
+    return acc
+
+
+def sweep_plane(data, table, padval=0, n_out=None):
+    """plane[d, t] = sum_c X(c, t + table[d, c]), t < n_out.  Default n_out =
+    N - max(0, max table): every row is then the prefix of the reference's
+    dedisperse(trim=True) series."""
+    data = np.asarray(data, dtype=np.float64)
+    N = data.shape[1]
+    if n_out is None:
+        n_out = N - max(0, int(np.max(table)))
+    return np.array([shifted_sum(data, table[d], padval)[:n_out] for d in range(table.shape[0])])

@@ -1,0 +1,108 @@
+"""ctypes binding of libpdd.so (the C ABI declared in include/pdd.h).
+
+The HIP library is REQUIRED: there is no CPU fallback anywhere in the product
+path.  If ``libpdd.so`` is missing, ``lib()`` raises ``PddLibraryMissing``.
+torch is imported first so that libpdd.so binds to the HIP runtime torch has
+already loaded (both carry the SONAME ``libamdhip64.so.7``): device pointers
+and stream handles are shared with torch.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime before libpdd.so)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpdd.so")
+
+# element types / modes (include/pdd.h)
+F32, U8, U16 = 0, 1, 2
+PAD_VALUE, PAD_ROTATE = 0, 1
+STAT_MEAN, STAT_MEDIAN = 0, 1
+LAYOUT_TIME_MAJOR, LAYOUT_CHAN_MAJOR = 0, 1
+
+# every symbol include/pdd.h declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "pdd_version", "pdd_last_error", "pdd_sync", "pdd_corner_turn", "pdd_convert_f32",
+    "pdd_channel_stats", "pdd_shift_pad", "pdd_shift_group_sum", "pdd_downsample",
+    "pdd_zero_dm", "pdd_sweep_plan_create", "pdd_sweep_execute", "pdd_sweep_plan_info",
+    "pdd_sweep_plan_destroy",
+)
+
+
+class PddLibraryMissing(RuntimeError):
+    pass
+
+
+class PddError(RuntimeError):
+    pass
+
+
+_lib = None
+
+_vp, _i64, _int = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+_SIGS = {
+    "pdd_version": ([], _int),
+    "pdd_last_error": ([], ctypes.c_char_p),
+    "pdd_sync": ([_vp], _int),
+    "pdd_corner_turn": ([_vp, _int, _i64, _i64, _i64, _vp, _int, _i64, _vp], _int),
+    "pdd_convert_f32": ([_vp, _int, _i64, _i64, _i64, _vp, _i64, _vp], _int),
+    "pdd_channel_stats": ([_vp, _i64, _i64, _i64, _int, _vp, _vp], _int),
+    "pdd_shift_pad": ([_vp, _i64, _i64, _i64, _vp, _int, _vp, _vp, _i64, _i64, _vp], _int),
+    "pdd_shift_group_sum": ([_vp, _i64, _i64, _i64, _vp, _int, _vp, _i64, _vp, _i64, _i64, _vp],
+                            _int),
+    "pdd_downsample": ([_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp], _int),
+    "pdd_zero_dm": ([_vp, _int, _i64, _i64, _i64, _int, _vp, _i64, _vp], _int),
+    "pdd_sweep_plan_create": ([_vp, _i64, _i64, _int, ctypes.POINTER(_vp)], _int),
+    "pdd_sweep_execute": ([_vp, _vp, _i64, _i64, _int, _vp, _vp, _i64, _i64, _vp], _int),
+    "pdd_sweep_plan_info": ([_vp, _vp], _int),
+    "pdd_sweep_plan_destroy": ([_vp], _int),
+}
+
+
+def lib():
+    """Load (once) and return the ctypes handle of libpdd.so."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PddLibraryMissing(
+                "libpdd.so not found at %s: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'`" % LIB_PATH)
+        h = ctypes.CDLL(LIB_PATH)
+        for name, (argtypes, restype) in _SIGS.items():
+            fn = getattr(h, name)
+            fn.argtypes = argtypes
+            fn.restype = restype
+        _lib = h
+    return _lib
+
+
+def check(status, what):
+    if status != 0:
+        msg = lib().pdd_last_error()
+        raise PddError("%s failed (status %d): %s" % (what, status,
+                                                      msg.decode() if msg else "?"))
+
+
+def call(name, *args):
+    check(getattr(lib(), name)(*args), name)
+
+
+def ptr(t):
+    """Device pointer of a CUDA tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise PddError("expected a device tensor, got one on %s" % t.device)
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise PddError("pypulsar_amd needs a ROCm GPU (torch.cuda.is_available() is False); "
+                       "there is no CPU fallback")
+    lib()

@@ -1,0 +1,457 @@
+// libpdd: single-pass (HBM-bound) kernels of the Spectra hot path, gfx950.
+//
+// Every kernel here reads its input once and writes its output once; they are
+// bounded by HBM (≈8 TB/s spec).  Algorithmic bytes per launch are documented
+// in DESIGN.md §Kernels.  Coalescing: consecutive lanes always touch
+// consecutive samples of one channel row (wave-strided, 64 lanes x 4 B).
+#include <cmath>
+#include <cstdarg>
+#include <cstring>
+
+#include "pdd_internal.h"
+
+namespace pdd {
+
+static thread_local char g_err[512] = {0};
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+// ---------------------------------------------------------------- loaders
+template <typename T>
+__device__ __forceinline__ float to_f32(T v) { return static_cast<float>(v); }
+
+// ---------------------------------------------------------------- corner turn
+// [nspec][nchan] -> [nchan][nspec] through a 64x65 LDS tile (padding breaks
+// the power-of-two column stride on the transposed read).
+template <typename InT, typename OutT>
+__global__ __launch_bounds__(256) void k_corner_turn(const InT* __restrict__ in, int64_t nspec,
+                                                     int64_t nchan, int64_t ld_in,
+                                                     OutT* __restrict__ out, int64_t ld_out,
+                                                     int64_t tiles_c) {
+  __shared__ OutT tile[64][65];
+  const int64_t tt = blockIdx.x / tiles_c, tc = blockIdx.x % tiles_c;
+  const int64_t t0 = tt * 64, c0 = tc * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t t = t0 + i, c = c0 + tx;
+    if (t < nspec && c < nchan) tile[i][tx] = static_cast<OutT>(in[t * ld_in + c]);
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t c = c0 + i, t = t0 + tx;
+    if (t < nspec && c < nchan) out[c * ld_out + t] = tile[tx][i];
+  }
+}
+
+template <typename InT>
+__global__ __launch_bounds__(256) void k_convert(const InT* __restrict__ in, int64_t rows,
+                                                 int64_t cols, int64_t ld_in,
+                                                 float* __restrict__ out, int64_t ld_out) {
+  const int64_t total = rows * cols;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / cols, c = i % cols;
+    out[r * ld_out + c] = to_f32(in[r * ld_in + c]);
+  }
+}
+
+// ---------------------------------------------------------------- reductions
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  return v;
+}
+
+// Per-channel mean in float64 (one workgroup per channel).
+__global__ __launch_bounds__(256) void k_channel_mean(const float* __restrict__ x, int64_t N,
+                                                      int64_t ld, float* __restrict__ out) {
+  __shared__ double part[4];
+  const float* row = x + (int64_t)blockIdx.x * ld;
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < N; i += 256) s += (double)row[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = (float)(((part[0] + part[1]) + (part[2] + part[3])) / (double)N);
+}
+
+// Orderable key of a float (total order for non-NaN values).
+__device__ __forceinline__ uint32_t fkey(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float fkey_inv(uint32_t k) {
+  uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  return __uint_as_float(u);
+}
+
+// k-th smallest of a row by 4 passes of 8-bit radix selection (LDS histogram).
+__device__ float radix_select_row(const float* __restrict__ row, int64_t N, int64_t k,
+                                  uint32_t* hist, uint32_t* shared_state) {
+  uint32_t prefix = 0, mask = 0;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < N; i += blockDim.x) {
+      const uint32_t key = fkey(row[i]);
+      if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t kk = k;
+      uint32_t d = 0;
+      for (; d < 256; ++d) {
+        if (kk < (int64_t)hist[d]) break;
+        kk -= hist[d];
+      }
+      shared_state[0] = d;
+      shared_state[1] = (uint32_t)kk;
+    }
+    __syncthreads();
+    const uint32_t d = shared_state[0];
+    k = shared_state[1];
+    prefix |= d << shift;
+    mask |= 255u << shift;
+    __syncthreads();
+  }
+  return fkey_inv(prefix);
+}
+
+// Per-channel median with numpy semantics (mean of the two middle values when
+// N is even).  One workgroup per channel.
+__global__ __launch_bounds__(256) void k_channel_median(const float* __restrict__ x, int64_t N,
+                                                        int64_t ld, float* __restrict__ out) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t st[2];
+  const float* row = x + (int64_t)blockIdx.x * ld;
+  const float hi = radix_select_row(row, N, N / 2, hist, st);
+  float med = hi;
+  if ((N & 1) == 0) {
+    const float lo = radix_select_row(row, N, N / 2 - 1, hist, st);
+    med = (float)(((double)lo + (double)hi) * 0.5);
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = med;
+}
+
+// ---------------------------------------------------------------- shift / pad
+// out[c][t] = X(c, t + bins[c]).  Block = 1024 consecutive outputs of one
+// channel; lane-consecutive samples per wave instruction.
+__global__ __launch_bounds__(256) void k_shift_pad(const float* __restrict__ x, int64_t N,
+                                                   int64_t ld, const int32_t* __restrict__ bins,
+                                                   int pad_mode, const float* __restrict__ padvals,
+                                                   float* __restrict__ out, int64_t ld_out,
+                                                   int64_t n_out, int64_t tiles) {
+  const int64_t c = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const float* row = x + c * ld;
+  float* orow = out + c * ld_out;
+  int64_t b = bins[c];
+  if (pad_mode == PDD_PAD_ROTATE) b = ((b % N) + N) % N;
+  const float pad = (pad_mode == PDD_PAD_VALUE) ? padvals[c] : 0.f;
+  const int64_t t0 = tile * 1024 + (threadIdx.x >> 6) * 256 + (threadIdx.x & 63);
+  float v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t t = t0 + 64 * k;
+    v[k] = (t < n_out) ? fetch_padded(row, t + b, N, pad_mode, pad) : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t t = t0 + 64 * k;
+    if (t < n_out) orow[t] = v[k];
+  }
+}
+
+// ---------------------------------------------------------------- shift + group sum
+// out[g][t] = sum_{c in group g} X(c, t + bins[c]).  Block = 256 outputs of
+// one group; wave w sums channels c = w, w+4, ... of the group in float64,
+// then the 4 partials are added in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void k_shift_group_sum(
+    const float* __restrict__ x, int64_t N, int64_t ld, const int32_t* __restrict__ bins,
+    int pad_mode, const float* __restrict__ padvals, int64_t cps, float* __restrict__ out,
+    int64_t ld_out, int64_t n_out, int64_t tiles) {
+  __shared__ double part[4][256];
+  const int64_t g = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t t0 = tile * 256 + lane;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t ci = w; ci < cps; ci += 4) {
+    const int64_t c = g * cps + ci;
+    const float* row = x + c * ld;
+    int64_t b = bins ? (int64_t)bins[c] : 0;
+    if (pad_mode == PDD_PAD_ROTATE) b = ((b % N) + N) % N;
+    const float pad = (pad_mode == PDD_PAD_VALUE && padvals) ? padvals[c] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t t = t0 + 64 * k;
+      if (t < n_out) acc[k] += (double)fetch_padded(row, t + b, N, pad_mode, pad);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) part[w][lane + 64 * k] = acc[k];
+  __syncthreads();
+  const int64_t t = tile * 256 + threadIdx.x;
+  if (t < n_out) {
+    const int i = threadIdx.x;
+    out[g * ld_out + t] = (float)((part[0][i] + part[1][i]) + (part[2][i] + part[3][i]));
+  }
+}
+
+// ---------------------------------------------------------------- downsample
+__global__ __launch_bounds__(256) void k_downsample(const float* __restrict__ x, int64_t ld,
+                                                    int64_t factor, int64_t nout,
+                                                    float* __restrict__ out, int64_t ld_out,
+                                                    int64_t tiles) {
+  const int64_t c = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const int64_t j = tile * 256 + threadIdx.x;
+  if (j >= nout) return;
+  const float* p = x + c * ld + j * factor;
+  double s = 0.0;
+  for (int64_t k = 0; k < factor; ++k) s += (double)p[k];
+  out[c * ld_out + j] = (float)s;
+}
+
+// ---------------------------------------------------------------- zero-DM
+// Integer data: avg = rint(float64(sum)/nchan) cast to the dtype, out = x - avg
+// modulo 2^nbits (bin/zero_dm_filter.py:35-39).  float32: float32 mean.
+template <typename T>
+__device__ __forceinline__ T zd_apply(T v, double mean) {
+  if constexpr (sizeof(T) == 4) {
+    return v - (float)mean;
+  } else {
+    const uint32_t a = (uint32_t)rint(mean);
+    return (T)((uint32_t)v - a);
+  }
+}
+
+// one wave per spectrum, time-major [nspec][nchan]
+template <typename T>
+__global__ __launch_bounds__(256) void k_zero_dm_tm(const T* __restrict__ in, int64_t nspec,
+                                                    int64_t nchan, int64_t ld,
+                                                    T* __restrict__ out, int64_t ld_out) {
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (s >= nspec) return;
+  const T* row = in + s * ld;
+  double mean;
+  if constexpr (sizeof(T) == 4) {
+    double acc = 0.0;
+    for (int64_t c = lane; c < nchan; c += 64) acc += (double)row[c];
+    acc = wave_sum(acc);
+    acc = __shfl(acc, 0, 64);
+    mean = (double)((float)acc / (float)nchan);
+  } else {
+    unsigned long long acc = 0;
+    for (int64_t c = lane; c < nchan; c += 64) acc += (unsigned long long)row[c];
+    acc = wave_sum_u64(acc);
+    acc = __shfl(acc, 0, 64);
+    mean = (double)acc / (double)nchan;
+  }
+  T* orow = out + s * ld_out;
+  for (int64_t c = lane; c < nchan; c += 64) orow[c] = zd_apply<T>(row[c], mean);
+}
+
+// one thread per spectrum, channel-major [nchan][nspec] (Spectra layout)
+template <typename T>
+__global__ __launch_bounds__(256) void k_zero_dm_cm(const T* __restrict__ in, int64_t nspec,
+                                                    int64_t nchan, int64_t ld,
+                                                    T* __restrict__ out, int64_t ld_out) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= nspec) return;
+  double mean;
+  if constexpr (sizeof(T) == 4) {
+    double acc = 0.0;
+    for (int64_t c = 0; c < nchan; ++c) acc += (double)in[c * ld + t];
+    mean = (double)((float)acc / (float)nchan);
+  } else {
+    unsigned long long acc = 0;
+    for (int64_t c = 0; c < nchan; ++c) acc += (unsigned long long)in[c * ld + t];
+    mean = (double)acc / (double)nchan;
+  }
+  for (int64_t c = 0; c < nchan; ++c) out[c * ld_out + t] = zd_apply<T>(in[c * ld + t], mean);
+}
+
+static int grid_1d(int64_t n, int per_block = 256) {
+  int64_t g = cdiv(n, per_block);
+  if (g > 2048 * 8) g = 2048 * 8;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace pdd
+
+using namespace pdd;
+
+extern "C" {
+
+int pdd_version(void) { return 1; }
+
+const char* pdd_last_error(void) { return pdd::g_err; }
+
+int pdd_sync(void* stream) {
+  PDD_HIP(hipStreamSynchronize(as_stream(stream)));
+  return 0;
+}
+
+int pdd_corner_turn(const void* in, int in_dtype, int64_t nspec, int64_t nchan, int64_t ld_in,
+                    void* out, int out_dtype, int64_t ld_out, void* stream) {
+  PDD_REQUIRE(in && out, "pdd_corner_turn: null pointer");
+  PDD_REQUIRE(nspec >= 0 && nchan >= 0 && ld_in >= nchan && ld_out >= nspec,
+              "pdd_corner_turn: bad shape nspec=%lld nchan=%lld ld_in=%lld ld_out=%lld",
+              (long long)nspec, (long long)nchan, (long long)ld_in, (long long)ld_out);
+  if (nspec == 0 || nchan == 0) return 0;
+  const int64_t tiles_c = cdiv(nchan, 64);
+  const int64_t blocks = cdiv(nspec, 64) * tiles_c;
+  PDD_REQUIRE(blocks < (1ll << 31), "pdd_corner_turn: too large");
+  hipStream_t s = as_stream(stream);
+#define CT(IT, OT)                                                                           \
+  k_corner_turn<IT, OT><<<(unsigned)blocks, 256, 0, s>>>((const IT*)in, nspec, nchan, ld_in, \
+                                                         (OT*)out, ld_out, tiles_c)
+  if (out_dtype == PDD_F32) {
+    if (in_dtype == PDD_U8) CT(uint8_t, float);
+    else if (in_dtype == PDD_U16) CT(uint16_t, float);
+    else if (in_dtype == PDD_F32) CT(float, float);
+    else PDD_REQUIRE(false, "pdd_corner_turn: bad in_dtype %d", in_dtype);
+  } else {
+    PDD_REQUIRE(out_dtype == in_dtype, "pdd_corner_turn: out dtype must be F32 or the input dtype");
+    if (in_dtype == PDD_U8) CT(uint8_t, uint8_t);
+    else if (in_dtype == PDD_U16) CT(uint16_t, uint16_t);
+    else PDD_REQUIRE(false, "pdd_corner_turn: bad in_dtype %d", in_dtype);
+  }
+#undef CT
+  PDD_LAUNCHED();
+  return 0;
+}
+
+int pdd_convert_f32(const void* in, int in_dtype, int64_t rows, int64_t cols, int64_t ld_in,
+                    float* out, int64_t ld_out, void* stream) {
+  PDD_REQUIRE(in && out, "pdd_convert_f32: null pointer");
+  PDD_REQUIRE(rows >= 0 && cols >= 0 && ld_in >= cols && ld_out >= cols,
+              "pdd_convert_f32: bad shape");
+  if (rows == 0 || cols == 0) return 0;
+  const int g = grid_1d(rows * cols);
+  hipStream_t s = as_stream(stream);
+  if (in_dtype == PDD_U8)
+    k_convert<uint8_t><<<g, 256, 0, s>>>((const uint8_t*)in, rows, cols, ld_in, out, ld_out);
+  else if (in_dtype == PDD_U16)
+    k_convert<uint16_t><<<g, 256, 0, s>>>((const uint16_t*)in, rows, cols, ld_in, out, ld_out);
+  else if (in_dtype == PDD_F32)
+    k_convert<float><<<g, 256, 0, s>>>((const float*)in, rows, cols, ld_in, out, ld_out);
+  else
+    PDD_REQUIRE(false, "pdd_convert_f32: bad dtype %d", in_dtype);
+  PDD_LAUNCHED();
+  return 0;
+}
+
+int pdd_channel_stats(const float* x, int64_t C, int64_t N, int64_t ld, int stat, float* out,
+                      void* stream) {
+  PDD_REQUIRE(x && out, "pdd_channel_stats: null pointer");
+  PDD_REQUIRE(C >= 0 && N > 0 && ld >= N, "pdd_channel_stats: bad shape");
+  PDD_REQUIRE(C < (1ll << 31), "pdd_channel_stats: too many channels");
+  if (C == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  if (stat == PDD_STAT_MEAN)
+    k_channel_mean<<<(unsigned)C, 256, 0, s>>>(x, N, ld, out);
+  else if (stat == PDD_STAT_MEDIAN)
+    k_channel_median<<<(unsigned)C, 256, 0, s>>>(x, N, ld, out);
+  else
+    PDD_REQUIRE(false, "pdd_channel_stats: bad stat %d", stat);
+  PDD_LAUNCHED();
+  return 0;
+}
+
+int pdd_shift_pad(const float* x, int64_t C, int64_t N, int64_t ld, const int32_t* bins,
+                  int pad_mode, const float* padvals, float* out, int64_t ld_out, int64_t n_out,
+                  void* stream) {
+  PDD_REQUIRE(x && out && bins, "pdd_shift_pad: null pointer");
+  PDD_REQUIRE(x != out, "pdd_shift_pad: out must not alias x");
+  PDD_REQUIRE(C >= 0 && N > 0 && ld >= N && n_out >= 0 && ld_out >= n_out,
+              "pdd_shift_pad: bad shape");
+  PDD_REQUIRE(pad_mode == PDD_PAD_ROTATE || (pad_mode == PDD_PAD_VALUE && padvals),
+              "pdd_shift_pad: bad pad mode %d", pad_mode);
+  if (C == 0 || n_out == 0) return 0;
+  const int64_t tiles = cdiv(n_out, 1024);
+  PDD_REQUIRE(C * tiles < (1ll << 31), "pdd_shift_pad: too large");
+  k_shift_pad<<<(unsigned)(C * tiles), 256, 0, as_stream(stream)>>>(x, N, ld, bins, pad_mode,
+                                                                    padvals, out, ld_out, n_out,
+                                                                    tiles);
+  PDD_LAUNCHED();
+  return 0;
+}
+
+int pdd_shift_group_sum(const float* x, int64_t C, int64_t N, int64_t ld, const int32_t* bins,
+                        int pad_mode, const float* padvals, int64_t nsub, float* out,
+                        int64_t ld_out, int64_t n_out, void* stream) {
+  PDD_REQUIRE(x && out, "pdd_shift_group_sum: null pointer");
+  PDD_REQUIRE(nsub > 0 && C % nsub == 0, "pdd_shift_group_sum: nsub must divide C");
+  PDD_REQUIRE(C >= 0 && N > 0 && ld >= N && n_out >= 0 && ld_out >= n_out,
+              "pdd_shift_group_sum: bad shape");
+  PDD_REQUIRE(pad_mode == PDD_PAD_ROTATE || pad_mode == PDD_PAD_VALUE,
+              "pdd_shift_group_sum: bad pad mode %d", pad_mode);
+  if (C == 0 || n_out == 0) return 0;
+  const int64_t tiles = cdiv(n_out, 256);
+  PDD_REQUIRE(nsub * tiles < (1ll << 31), "pdd_shift_group_sum: too large");
+  k_shift_group_sum<<<(unsigned)(nsub * tiles), 256, 0, as_stream(stream)>>>(
+      x, N, ld, bins, pad_mode, padvals, C / nsub, out, ld_out, n_out, tiles);
+  PDD_LAUNCHED();
+  return 0;
+}
+
+int pdd_downsample(const float* x, int64_t C, int64_t N, int64_t ld, int64_t factor, float* out,
+                   int64_t ld_out, void* stream) {
+  PDD_REQUIRE(x && out, "pdd_downsample: null pointer");
+  PDD_REQUIRE(factor >= 1 && C >= 0 && N >= 0 && ld >= N, "pdd_downsample: bad shape");
+  const int64_t nout = N / factor;
+  PDD_REQUIRE(ld_out >= nout, "pdd_downsample: ld_out too small");
+  if (C == 0 || nout == 0) return 0;
+  const int64_t tiles = cdiv(nout, 256);
+  PDD_REQUIRE(C * tiles < (1ll << 31), "pdd_downsample: too large");
+  k_downsample<<<(unsigned)(C * tiles), 256, 0, as_stream(stream)>>>(x, ld, factor, nout, out,
+                                                                     ld_out, tiles);
+  PDD_LAUNCHED();
+  return 0;
+}
+
+int pdd_zero_dm(const void* in, int dtype, int64_t nspec, int64_t nchan, int64_t ld, int layout,
+                void* out, int64_t ld_out, void* stream) {
+  PDD_REQUIRE(in && out, "pdd_zero_dm: null pointer");
+  PDD_REQUIRE(nspec >= 0 && nchan > 0, "pdd_zero_dm: bad shape");
+  if (nspec == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  if (layout == PDD_LAYOUT_TIME_MAJOR) {
+    PDD_REQUIRE(ld >= nchan && ld_out >= nchan, "pdd_zero_dm: bad ld");
+    const int64_t g = cdiv(nspec, 4);
+    PDD_REQUIRE(g < (1ll << 31), "pdd_zero_dm: too large");
+#define ZT(T) k_zero_dm_tm<T><<<(unsigned)g, 256, 0, s>>>((const T*)in, nspec, nchan, ld, (T*)out, ld_out)
+    if (dtype == PDD_U8) ZT(uint8_t);
+    else if (dtype == PDD_U16) ZT(uint16_t);
+    else if (dtype == PDD_F32) ZT(float);
+    else PDD_REQUIRE(false, "pdd_zero_dm: bad dtype %d", dtype);
+#undef ZT
+  } else if (layout == PDD_LAYOUT_CHAN_MAJOR) {
+    PDD_REQUIRE(ld >= nspec && ld_out >= nspec, "pdd_zero_dm: bad ld");
+    const int64_t g = cdiv(nspec, 256);
+#define ZC(T) k_zero_dm_cm<T><<<(unsigned)g, 256, 0, s>>>((const T*)in, nspec, nchan, ld, (T*)out, ld_out)
+    if (dtype == PDD_U8) ZC(uint8_t);
+    else if (dtype == PDD_U16) ZC(uint16_t);
+    else if (dtype == PDD_F32) ZC(float);
+    else PDD_REQUIRE(false, "pdd_zero_dm: bad dtype %d", dtype);
+#undef ZC
+  } else {
+    PDD_REQUIRE(false, "pdd_zero_dm: bad layout %d", layout);
+  }
+  PDD_LAUNCHED();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,300 @@
+"""Device-resident ``Spectra``: the drop-in for pypulsar's formats/spectra.py.
+
+Same constructor, attributes, method names, argument meanings and assertion
+behaviour as the reference class (formats/spectra.py:8-351).  The data live in
+HBM as float32 ``[numchans, numspectra]`` (a strided view of a device buffer so
+``trim`` never copies); every hot-path method runs a hand-written HIP kernel
+of libpdd.so through the C ABI (include/pdd.h).  There is no CPU fallback:
+without a GPU or without libpdd.so the methods raise.
+
+Documented differences from the reference:
+  * float32 on device instead of float64 (parity: integer-valued data and
+    integer pads are bit-exact; otherwise 1e-5 relative);
+  * ``.data`` is a float64 host *snapshot* (a device->host copy), so writing
+    into ``spectra.data[...]`` does not change the Spectra: use
+    ``spectra[key] = value`` (``__setitem__``) or assign ``spectra.data = arr``;
+  * ``get_chan``/``get_spectrum`` likewise return host copies.
+"""
+import copy
+
+import numpy as np
+import torch
+
+from .. import _lib
+from .._lib import call, ptr, stream_ptr
+from .. import delays as _delays
+
+
+def _np_dtype_code(dt):
+    if dt == np.uint8:
+        return _lib.U8
+    if dt == np.uint16:
+        return _lib.U16
+    if dt == np.float32:
+        return _lib.F32
+    return None
+
+
+def _torch_dtype_code(dt):
+    return {torch.uint8: _lib.U8, torch.float32: _lib.F32}.get(dt)
+
+
+def upload_f32(data):
+    """Copy a [C, N] array (numpy, any order/dtype, or torch) to a new
+    contiguous float32 device tensor through libpdd (corner turn for the
+    transposed filterbank layout, conversion for u8/u16/f32).  Also returns
+    the raw 8-bit [C, N] device copy when the input is uint8 (for the 8-bit
+    sweep kernel), else None."""
+    _lib.require_gpu()
+    dev = torch.device("cuda")
+    if isinstance(data, torch.Tensor):
+        t = data
+        if t.dim() != 2:
+            raise ValueError("data must be 2-D")
+        C, N = t.shape
+        if t.dtype not in (torch.uint8, torch.float32):
+            t = t.to(torch.float32)
+        t = t.to(dev)
+        code = _torch_dtype_code(t.dtype)
+        out = torch.empty((C, N), dtype=torch.float32, device=dev)
+        raw8 = None
+        if t.stride(1) == 1:
+            call("pdd_convert_f32", ptr(t), code, C, N, t.stride(0), ptr(out), N, stream_ptr())
+            if t.dtype == torch.uint8:
+                raw8 = t.contiguous().clone()
+        elif t.stride(0) == 1:  # transposed [N, C] storage
+            call("pdd_corner_turn", ptr(t), code, N, C, t.stride(1), ptr(out), _lib.F32, N,
+                 stream_ptr())
+            if t.dtype == torch.uint8:
+                raw8 = t.contiguous()
+        else:
+            tc = t.contiguous()
+            call("pdd_convert_f32", ptr(tc), code, C, N, N, ptr(out), N, stream_ptr())
+            if t.dtype == torch.uint8:
+                raw8 = tc.clone()
+        return out, raw8
+
+    a = np.asarray(data)
+    if a.ndim != 2:
+        raise ValueError("data must be 2-D")
+    C, N = a.shape
+    code = _np_dtype_code(a.dtype)
+    if code is None:
+        a = a.astype(np.float32)
+        code = _lib.F32
+    out = torch.empty((C, N), dtype=torch.float32, device=dev)
+    raw8 = None
+    if C == 0 or N == 0:
+        return out, None
+    if a.T.flags.c_contiguous and not a.flags.c_contiguous:
+        # the layout filterbank.get_spectra hands over: data.T of an [N, C] block
+        src = torch.from_numpy(np.ascontiguousarray(a.T)).to(dev, non_blocking=False)
+        call("pdd_corner_turn", ptr(src), code, N, C, C, ptr(out), _lib.F32, N, stream_ptr())
+        if code == _lib.U8:
+            raw8 = torch.empty((C, N), dtype=torch.uint8, device=dev)
+            call("pdd_corner_turn", ptr(src), code, N, C, C, ptr(raw8), _lib.U8, N, stream_ptr())
+    else:
+        src = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        call("pdd_convert_f32", ptr(src), code, C, N, N, ptr(out), N, stream_ptr())
+        if code == _lib.U8:
+            raw8 = src
+    return out, raw8
+
+
+def _pad_args(x, padval):
+    """(pad_mode, padvals device tensor or None) for a [C, N] float32 view,
+    the semantics of spectra.py:81-94."""
+    C = x.shape[0]
+    if isinstance(padval, str):
+        if padval == "rotate":
+            return _lib.PAD_ROTATE, None
+        if padval in ("mean", "median"):
+            stat = _lib.STAT_MEAN if padval == "mean" else _lib.STAT_MEDIAN
+            pv = torch.empty(C, dtype=torch.float32, device=x.device)
+            call("pdd_channel_stats", ptr(x), C, x.shape[1], x.stride(0), stat, ptr(pv),
+                 stream_ptr())
+            return _lib.PAD_VALUE, pv
+        raise ValueError("padval must be a number, 'mean', 'median' or 'rotate'")
+    pv = torch.full((C,), float(padval), dtype=torch.float32, device=x.device)
+    return _lib.PAD_VALUE, pv
+
+
+def _bins_dev(bins, device):
+    return torch.from_numpy(_delays.to_int32(bins)).to(device)
+
+
+class Spectra(object):
+    """A [numchans, numspectra] block of filterbank data on the GPU."""
+
+    def __init__(self, freqs, dt, data, starttime=0, dm=0):
+        self.numchans, self.numspectra = data.shape
+        assert len(freqs) == self.numchans
+        self.freqs = freqs
+        self._x, self._raw8 = upload_f32(data)
+        self.dt = dt
+        self.starttime = starttime
+        self.dm = 0  # the reference ignores the dm argument (spectra.py:37)
+
+    # ------------------------------------------------------------ data access
+    @property
+    def device_data(self):
+        """The float32 [numchans, numspectra] device view (no copy)."""
+        return self._x
+
+    @property
+    def data(self):
+        return self._x.to(torch.float64).cpu().numpy()
+
+    @data.setter
+    def data(self, value):
+        self._x, self._raw8 = upload_f32(value)
+        self.numchans, self.numspectra = self._x.shape
+
+    def _set(self, x):
+        self._x = x
+        self._raw8 = None
+
+    def __str__(self):
+        return str(self.data)
+
+    def __getitem__(self, key):
+        return self.data[key]
+
+    def __setitem__(self, key, value):
+        if not isinstance(value, torch.Tensor):
+            value = torch.as_tensor(np.asarray(value, dtype=np.float32))
+        self._x[key] = value.to(device=self._x.device, dtype=torch.float32)
+        self._raw8 = None
+
+    def get_chan(self, channum):
+        return self.data[channum, :]
+
+    def get_spectrum(self, specnum):
+        return self.data[:, specnum]
+
+    def __deepcopy__(self, memo):
+        other = copy.copy(self)
+        other._x = self._x.clone()
+        other._raw8 = None if self._raw8 is None else self._raw8.clone()
+        other.freqs = copy.deepcopy(self.freqs, memo)
+        return other
+
+    # ------------------------------------------------------------ hot path
+    def shift_channels(self, bins, padval=0):
+        """Shift each channel left by bins[c] and pad (spectra.py:54-94)."""
+        assert self.numchans == len(bins)
+        x = self._x
+        C, N = x.shape
+        if C == 0 or N == 0:
+            return
+        mode, pv = _pad_args(x, padval)
+        out = torch.empty((C, N), dtype=torch.float32, device=x.device)
+        b = _bins_dev(bins, x.device)
+        call("pdd_shift_pad", ptr(x), C, N, x.stride(0), ptr(b), mode, ptr(pv), ptr(out), N, N,
+             stream_ptr())
+        self._set(out)
+
+    def subband(self, nsub, subdm=None, padval=0):
+        """Shift within subbands at subdm and sum them (spectra.py:96-138).
+        ``self.dm`` is not changed (as in the reference)."""
+        assert (self.numchans % nsub) == 0
+        assert (subdm is None) or (subdm >= 0)
+        freqs = np.asarray(self.freqs, dtype=np.float64)
+        _, _, ctr = _delays.subband_layout(freqs, nsub)
+        x = self._x
+        C, N = x.shape
+        out = torch.empty((nsub, N), dtype=torch.float32, device=x.device)
+        if N > 0:
+            if subdm is not None:
+                bins = _delays.subband_bins(subdm, freqs, self.dt, nsub, cur_dm=self.dm)
+                b = _bins_dev(bins, x.device)
+                mode, pv = _pad_args(x, padval)
+            else:
+                b, mode, pv = None, _lib.PAD_VALUE, None
+            call("pdd_shift_group_sum", ptr(x), C, N, x.stride(0), ptr(b), mode, ptr(pv), nsub,
+                 ptr(out), N, N, stream_ptr())
+        self._set(out)
+        self.freqs = ctr
+        self.numchans = nsub
+
+    def dedisperse(self, dm=0, padval=0, trim=False):
+        """Shift channels by the delays of ``dm`` (spectra.py:229-260)."""
+        assert dm >= 0
+        bins = _delays.dedisperse_bins(dm, self.freqs, self.dt, cur_dm=self.dm)
+        self.shift_channels(bins, padval)
+        self.dm = dm
+        if trim:
+            ntrim = int(max(bins))
+            if ntrim > 0:
+                self._set(self._x[:, :max(0, self._x.shape[1] - ntrim)])
+                self.numspectra -= ntrim
+
+    def trim(self, bins=0):
+        """Drop ``bins`` samples from the end (or -bins from the start),
+        spectra.py:305-327 -- including the reference's numspectra arithmetic
+        for negative bins."""
+        assert bins < self.numspectra
+        if bins == 0:
+            return
+        elif bins > 0:
+            self._set(self._x[:, :-bins])
+            self.numspectra = self.numspectra - bins
+        elif bins < 0:
+            self._set(self._x[:, bins:])
+            self.numspectra = self.numspectra - bins
+            self.starttime = self.starttime + bins * self.dt
+
+    def downsample(self, factor=1, trim=True):
+        """Co-add ``factor`` adjacent samples (spectra.py:329-351)."""
+        assert trim or not (self.numspectra % factor)
+        new_num_spectra = self.numspectra // factor
+        self.trim(self.numspectra % factor)
+        x = self._x
+        C, N = x.shape
+        out = torch.empty((C, new_num_spectra), dtype=torch.float32, device=x.device)
+        if C and new_num_spectra:
+            call("pdd_downsample", ptr(x), C, N, x.stride(0), factor, ptr(out), new_num_spectra,
+                 stream_ptr())
+        self._set(out)
+        self.numspectra = new_num_spectra
+        self.dt = self.dt * factor
+
+    # ------------------------------------------------------------ fused extras
+    def sum_channels(self):
+        """Device float32 [numspectra] series = data.sum(axis=0)
+        (bin/waterfaller.py:140), float64 accumulation in the kernel."""
+        x = self._x
+        C, N = x.shape
+        out = torch.empty((1, N), dtype=torch.float32, device=x.device)
+        if N:
+            call("pdd_shift_group_sum", ptr(x), C, N, x.stride(0), None, _lib.PAD_VALUE, None, 1,
+                 ptr(out), N, N, stream_ptr())
+        return out[0]
+
+    def dedispersed_series(self, dm, padval=0, trim=True):
+        """Fused dedisperse(dm, padval, trim) + channel sum WITHOUT modifying
+        this Spectra: one pass over the data (pdd_shift_group_sum, nsub=1)."""
+        assert dm >= 0
+        bins = _delays.dedisperse_bins(dm, self.freqs, self.dt, cur_dm=self.dm)
+        x = self._x
+        C, N = x.shape
+        ntrim = int(max(bins)) if trim else 0
+        n_out = N - ntrim if ntrim > 0 else N
+        n_out = max(0, n_out)
+        out = torch.empty((1, max(1, n_out)), dtype=torch.float32, device=x.device)
+        if n_out:
+            mode, pv = _pad_args(x, padval)
+            b = _bins_dev(bins, x.device)
+            call("pdd_shift_group_sum", ptr(x), C, N, x.stride(0), ptr(b), mode, ptr(pv), 1,
+                 ptr(out), n_out, n_out, stream_ptr())
+        return out[0, :n_out]
+
+    def sweep(self, dms, padval=0, trim=True, plane=None):
+        """Batched DM-trial sweep of this Spectra (new executor): returns
+        the float32 device plane [len(dms), n_out], row d = the dedispersed
+        series of ``dedisperse(dms[d], padval, trim)``, truncated to the
+        common length (trim=True) or full length (trim=False)."""
+        from ..sweep import DMSweep
+        sw = DMSweep(dms, self.freqs, self.dt, cur_dm=self.dm,
+                     dtype="u8" if (self._raw8 is not None) else "f32")
+        return sw(self, padval=padval, trim=trim, out=plane)

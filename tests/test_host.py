@@ -1,0 +1,96 @@
+"""Host-side product logic (CPU only): bit-exact delay tables and the DDplan
+grid generator against the reference's golden fixtures."""
+import numpy as np
+import pytest
+
+from pypulsar_amd import delays
+from pypulsar_amd.utils import ddplan
+from conftest import band
+
+DT = 64e-6
+
+
+@pytest.mark.parametrize("C", [64, 1024, 4096])
+@pytest.mark.parametrize("tag", ["desc", "asc"])
+def test_dedisperse_bins_bit_exact(golden, C, tag):
+    key = "bins_C%d_%s" % (C, tag)
+    freqs = golden[key + "_freqs"]
+    assert np.array_equal(freqs, band(C, tag == "desc"))
+    for i, dm in enumerate(golden["bins_dms"]):
+        assert np.array_equal(delays.dedisperse_bins(dm, freqs, DT), golden[key][i])
+    # the vectorised [D, C] table must be bit-identical row by row
+    tab = delays.sweep_table(golden["bins_dms"], freqs, DT)
+    assert np.array_equal(tab, golden[key])
+
+
+def test_sweep_table_grid(golden):
+    tab = delays.sweep_table(golden["bins_grid_dms"], band(1024), DT)
+    assert np.array_equal(tab, golden["bins_grid"])
+
+
+def test_sweep_table_cur_dm():
+    freqs = band(256)
+    for cur in (0.0, 37.5, 100.0):
+        for dm in (0.0, 12.5, 50.0, 333.0):
+            row = delays.sweep_table([dm], freqs, DT, cur_dm=cur)[0]
+            assert np.array_equal(row, delays.dedisperse_bins(dm, freqs, DT, cur_dm=cur))
+
+
+@pytest.mark.parametrize("tag", ["desc", "asc"])
+@pytest.mark.parametrize("nsub", [8, 32])
+def test_subband_bins(golden, golden_meta, tag, nsub):
+    freqs = golden["sb_freqs_" + tag]
+    for si, subdm in enumerate(golden_meta["subdms"]):
+        if subdm is None:
+            continue
+        k = "sb_%s_n%d_s%d_p0" % (tag, nsub, si)
+        assert np.array_equal(delays.subband_bins(subdm, freqs, DT, nsub), golden[k + "_bins"])
+        _, _, ctr = delays.subband_layout(freqs, nsub)
+        assert np.array_equal(ctr, golden[k + "_freqs"])
+
+
+def test_known_answer_delay():
+    # k_DM = 1/0.000241 s MHz^2 / (pc cm^-3): DM 100 at 1000 MHz -> 0.41494 s
+    assert delays.delay_from_DM(100.0, 1000.0) == pytest.approx(100.0 / 241.0, rel=1e-15)
+    assert delays.delay_from_DM(100.0, np.array([0.0, -5.0]))[0] == 0.0
+    # guess_DMstep o dm_smear = identity (DDplan2b.py:447)
+    for dt_, bw, f in [(64e-6, 300.0, 1400.0), (1e-3, 10.0, 350.0)]:
+        dm = delays.guess_DMstep(dt_, bw, f)
+        assert delays.dm_smear(dm, bw, f) == pytest.approx(dt_, rel=1e-12)
+
+
+def test_int32_guard():
+    with pytest.raises(OverflowError):
+        delays.to_int32(np.array([2 ** 31]))
+
+
+@pytest.mark.parametrize("i", range(6))
+def test_ddplan_matches_reference(golden, golden_meta, i):
+    meta = golden_meta["ddplans"][i]
+    p = meta["params"]
+    obs = ddplan.Observation(p["dt"], p["fctr"], p["BW"], p["numchan"], p["numsamp"])
+    plan = obs.gen_ddplan(p["lo"], p["hi"], p["nsub"], p["res"])
+    assert len(plan.DDsteps) == len(meta["steps"])
+    for j, (st, ref) in enumerate(zip(plan.DDsteps, meta["steps"])):
+        assert st.loDM == ref["loDM"] and st.hiDM == ref["hiDM"] and st.dDM == ref["dDM"]
+        assert st.downsamp == ref["downsamp"] and st.numDMs == ref["numDMs"]
+        assert st.dsubDM == ref["dsubDM"] and st.numprepsub == ref["numprepsub"]
+        if p["nsub"]:
+            assert st.DMs_per_prepsub == ref["DMs_per_prepsub"]
+        assert st.BW_smearing == ref["BW_smearing"] and st.sub_smearing == ref["sub_smearing"]
+        assert np.array_equal(st.DMs, golden["ddplan%d_step%d_DMs" % (i, j)])
+        assert np.array_equal(st.tot_smear, golden["ddplan%d_step%d_totsmear" % (i, j)])
+    assert np.array_equal(plan.work_fracts, golden["ddplan%d_workfracts" % i])
+    assert plan.resolution == meta["resolution"]
+    assert str(plan) == meta["text"]
+
+
+def test_ddplan_subband_calls():
+    obs = ddplan.Observation(64e-6, 1400.0, 300.0, 4096)
+    plan = obs.gen_ddplan(0.0, 1000.0, 64, 0.5)
+    (step,) = plan.DDsteps
+    calls = step.subband_calls()
+    assert len(calls) == step.numprepsub == 40
+    assert all(len(d) == step.DMs_per_prepsub == 50 for _, d in calls)
+    assert np.array_equal(np.concatenate([d for _, d in calls]), step.DMs)
+    assert calls[0][0] == pytest.approx(0.5 * step.dsubDM)
