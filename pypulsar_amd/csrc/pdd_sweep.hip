@@ -25,6 +25,7 @@
 //  * blockIdx is remapped so the n_dblk DM blocks of one time tile run
 //    back to back on ONE XCD and re-read the tile's input from that XCD's L2.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 #include <vector>
@@ -56,20 +57,190 @@ __device__ __forceinline__ int64_t wrap_mod(int64_t s, int64_t N) {
   return r < 0 ? r + N : r;
 }
 
-template <bool U8, int S, int G, int DPW, int NW>
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+// Stage one channel of the striped image with the reference pad semantics
+// (register path: used for 8-bit data and for float32 channels whose window
+// leaves [0, N), i.e. edge tiles, pads and rotation).
+template <bool U8, int S, int Q, int NT>
+__device__ __forceinline__ void stage_channel_regs(typename ElemOf<U8, S>::type* dst,
+                                                   const void* xv, int64_t ld, int c, int64_t N,
+                                                   int64_t sb, int ne, bool inside, int pad_mode,
+                                                   const float* __restrict__ padvals) {
+  using E = typename ElemOf<U8, S>::type;
+  constexpr int WORDS = U8 ? S / 2 : S;
+  if constexpr (U8) {
+    const uint8_t* row = reinterpret_cast<const uint8_t*>(xv) + (int64_t)c * ld;
+    if (inside) {
+      const uint8_t* rb = row + sb;
+      for (int e = threadIdx.x; e < ne; e += NT) {
+        E v;
+#pragma unroll
+        for (int h = 0; h < WORDS; ++h)
+          set_w(v, h, (uint32_t)rb[e + (2 * h) * Q] | ((uint32_t)rb[e + (2 * h + 1) * Q] << 16));
+        dst[e] = v;
+      }
+    } else {
+      const uint32_t pv = (pad_mode == PDD_PAD_VALUE) ? (uint32_t)padvals[c] : 0u;
+      for (int e = threadIdx.x; e < ne; e += NT) {
+        E v;
+#pragma unroll
+        for (int h = 0; h < WORDS; ++h) {
+          uint32_t lo, hi;
+          const int64_t s0 = sb + e + (2 * h) * Q, s1 = s0 + Q;
+          if (pad_mode == PDD_PAD_ROTATE) {
+            lo = row[wrap_mod(s0, N)];
+            hi = row[wrap_mod(s1, N)];
+          } else {
+            lo = (s0 >= 0 && s0 < N) ? (uint32_t)row[s0] : pv;
+            hi = (s1 >= 0 && s1 < N) ? (uint32_t)row[s1] : pv;
+          }
+          set_w(v, h, lo | (hi << 16));
+        }
+        dst[e] = v;
+      }
+    }
+  } else {
+    const float* row = reinterpret_cast<const float*>(xv) + (int64_t)c * ld;
+    const float pv = (pad_mode == PDD_PAD_VALUE) ? padvals[c] : 0.f;
+    for (int e = threadIdx.x; e < ne; e += NT) {
+      E v;
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        const int64_t s = sb + e + k * Q;
+        float f;
+        if (inside) f = row[s];
+        else if (pad_mode == PDD_PAD_ROTATE) f = row[wrap_mod(s, N)];
+        else f = (s >= 0 && s < N) ? row[s] : pv;
+        set_w(v, k, __float_as_uint(f));
+      }
+      dst[e] = v;
+    }
+  }
+}
+
+// float32 channel fully inside [0, N): asynchronous LDS-DMA
+// (global_load_lds_dword) straight into the striped image.  One
+// wave-instruction writes 256 contiguous LDS bytes = 16 elements x 4 stripes;
+// lane l loads sample (e0 + l/4) of stripe l%4.  Elements past ne are filled
+// from a clamped (valid) address and never read.
+template <int Q, int NW>
+__device__ __forceinline__ int stage_channel_dma(uint4* dst, const float* rb, int ne, int w,
+                                                 int lane) {
+  // Issued through inline asm: hipcc would otherwise treat the DMA as a
+  // pending LDS write and put vmcnt(0) in front of every ds_read of the OTHER
+  // buffer.  The kernel waits for it explicitly (vmcnt(0) before the barrier
+  // that publishes the chunk).
+  const int nq = (ne + 15) >> 4;
+  const int k = lane & 3;
+  for (int q = w; q < nq; q += NW) {
+    const int e = min(q * 16 + (lane >> 2), ne - 1);
+    const float* src = rb + e + k * Q;
+    const uint32_t lds_addr = (uint32_t)(uintptr_t)(lds_void_t*)(dst + q * 16);
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dword %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
+        : "memory");
+  }
+  return w < nq ? (nq - 1 - w) / NW + 1 : 0;  // DMAs this wave issued
+}
+
+// s_waitcnt vmcnt(n) for a run-time n (the counter field is an immediate):
+// "all but the youngest n vector-memory operations of this wave are done".
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  n = __builtin_amdgcn_readfirstlane(n);
+  switch (n < 63 ? n : 63) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
+    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+    case 19: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); break;
+    case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 21: asm volatile("s_waitcnt vmcnt(21)" ::: "memory"); break;
+    case 22: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;
+    case 23: asm volatile("s_waitcnt vmcnt(23)" ::: "memory"); break;
+    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 25: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
+    case 26: asm volatile("s_waitcnt vmcnt(26)" ::: "memory"); break;
+    case 27: asm volatile("s_waitcnt vmcnt(27)" ::: "memory"); break;
+    case 28: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
+    case 29: asm volatile("s_waitcnt vmcnt(29)" ::: "memory"); break;
+    case 30: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
+    case 31: asm volatile("s_waitcnt vmcnt(31)" ::: "memory"); break;
+    case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+    case 33: asm volatile("s_waitcnt vmcnt(33)" ::: "memory"); break;
+    case 34: asm volatile("s_waitcnt vmcnt(34)" ::: "memory"); break;
+    case 35: asm volatile("s_waitcnt vmcnt(35)" ::: "memory"); break;
+    case 36: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
+    case 37: asm volatile("s_waitcnt vmcnt(37)" ::: "memory"); break;
+    case 38: asm volatile("s_waitcnt vmcnt(38)" ::: "memory"); break;
+    case 39: asm volatile("s_waitcnt vmcnt(39)" ::: "memory"); break;
+    case 40: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
+    case 41: asm volatile("s_waitcnt vmcnt(41)" ::: "memory"); break;
+    case 42: asm volatile("s_waitcnt vmcnt(42)" ::: "memory"); break;
+    case 43: asm volatile("s_waitcnt vmcnt(43)" ::: "memory"); break;
+    case 44: asm volatile("s_waitcnt vmcnt(44)" ::: "memory"); break;
+    case 45: asm volatile("s_waitcnt vmcnt(45)" ::: "memory"); break;
+    case 46: asm volatile("s_waitcnt vmcnt(46)" ::: "memory"); break;
+    case 47: asm volatile("s_waitcnt vmcnt(47)" ::: "memory"); break;
+    case 48: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
+    case 49: asm volatile("s_waitcnt vmcnt(49)" ::: "memory"); break;
+    case 50: asm volatile("s_waitcnt vmcnt(50)" ::: "memory"); break;
+    case 51: asm volatile("s_waitcnt vmcnt(51)" ::: "memory"); break;
+    case 52: asm volatile("s_waitcnt vmcnt(52)" ::: "memory"); break;
+    case 53: asm volatile("s_waitcnt vmcnt(53)" ::: "memory"); break;
+    case 54: asm volatile("s_waitcnt vmcnt(54)" ::: "memory"); break;
+    case 55: asm volatile("s_waitcnt vmcnt(55)" ::: "memory"); break;
+    case 56: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
+    case 57: asm volatile("s_waitcnt vmcnt(57)" ::: "memory"); break;
+    case 58: asm volatile("s_waitcnt vmcnt(58)" ::: "memory"); break;
+    case 59: asm volatile("s_waitcnt vmcnt(59)" ::: "memory"); break;
+    case 60: asm volatile("s_waitcnt vmcnt(60)" ::: "memory"); break;
+    case 61: asm volatile("s_waitcnt vmcnt(61)" ::: "memory"); break;
+    case 62: asm volatile("s_waitcnt vmcnt(62)" ::: "memory"); break;
+    case 63: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
+  }
+}
+
+template <bool U8, int S, int G, int DPW, int NW, int CC, int NBUF>
 __global__ __launch_bounds__(NW * 64) void k_sweep(
-    const void* __restrict__ xv, int64_t ld, int C, int64_t N, const int* __restrict__ tab,
+    const void* __restrict__ xv, int64_t ld, int C, int64_t N, const int* __restrict__ rel,
     int Dpad, int D, const int* __restrict__ bmin, const int* __restrict__ bspan, int pad_mode,
     const float* __restrict__ padvals, float* __restrict__ out, int64_t ld_out, int64_t n_out,
-    int cc, int stride, int n_tblk, int n_dblk) {
+    int dbg, int stride, int n_tblk, int n_dblk) {
+  constexpr int cc = CC;
   constexpr int Q = 64 * G;
   constexpr int TB = S * Q;
   constexpr int DB = NW * DPW;
   constexpr int NT = NW * 64;
   constexpr int WORDS = U8 ? S / 2 : S;  // 32-bit words per LDS element
+  constexpr bool DMA = !U8 && S == 4;
   using E = typename ElemOf<U8, S>::type;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   E* lds = reinterpret_cast<E*>(smem);
+  const int64_t buf_elems = (int64_t)cc * stride;  // one of the two chunk buffers
 
   // XCD-aware tile order: blocks b and b+8 share an XCD; give each XCD a
   // contiguous run of L so the DM blocks of one time tile share its L2.
@@ -79,10 +250,39 @@ __global__ __launch_bounds__(NW * 64) void k_sweep(
   const int L = (bid < full) ? (bid % 8) * (total / 8) + bid / 8 : bid;
   const int dblk = L % n_dblk, tblk = L / n_dblk;
   const int64_t t0 = (int64_t)tblk * TB;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // wave index as a scalar so the per-(channel, trial) offsets are fetched by
+  // scalar loads (one s_load per channel for the wave's DPW trials)
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   const int d0 = dblk * DB + w * DPW;
   const int* bmin_b = bmin + (int64_t)dblk * C;
   const int* bspan_b = bspan + (int64_t)dblk * C;
+
+  // stage chunk [c0, c0 + ncc) into buffer `b`; returns the number of
+  // LDS-DMA instructions this wave left in flight
+  auto stage = [&](int c0, int b) -> int {
+    const int ncc = min(cc, C - c0);
+    int ndma = 0;
+    E* base = lds + b * buf_elems;
+    for (int i = 0; i < ncc; ++i) {
+      const int c = c0 + i;
+      const int bm = bmin_b[c];
+      const int ne = Q + bspan_b[c];
+      const int64_t sb = t0 + bm;
+      const bool inside = (sb >= 0) && (sb + (int64_t)(S - 1) * Q + ne <= N);
+      E* dst = base + (int64_t)i * stride;
+      if constexpr (DMA) {
+        if (inside) {
+          ndma += stage_channel_dma<Q, NW>(reinterpret_cast<uint4*>(dst),
+                                           reinterpret_cast<const float*>(xv) + (int64_t)c * ld + sb,
+                                           ne, w, lane);
+          continue;
+        }
+      }
+      stage_channel_regs<U8, S, Q, NT>(dst, xv, ld, c, N, sb, ne, inside, pad_mode, padvals);
+    }
+    return ndma;
+  };
 
   float accf[DPW][G][S];
 #pragma unroll
@@ -102,72 +302,68 @@ __global__ __launch_bounds__(NW * 64) void k_sweep(
   }
   int since_flush = 0;
 
+  // Ring of NBUF channel-chunk buffers: chunks k+1 .. k+NBUF-1 are staged
+  // (LDS-DMA in flight for float32) while chunk k is accumulated.  One
+  // barrier per chunk; before it every wave waits with a COUNTED vmcnt that
+  // retires only chunk k's DMAs and keeps the younger chunks in flight.
+  int pend[NBUF];  // pend[s] = DMAs this wave has in flight for chunk k+s
+#pragma unroll
+  for (int s2 = 0; s2 < NBUF; ++s2) pend[s2] = 0;
+#pragma unroll
+  for (int s2 = 0; s2 < NBUF - 1; ++s2)
+    if (s2 * cc < C) pend[s2] = stage(s2 * cc, s2);
+  int cur = 0;
   for (int c0 = 0; c0 < C; c0 += cc) {
     const int ncc = min(cc, C - c0);
-    __syncthreads();
-    // ---- stage the chunk's channels into the striped LDS image
-    for (int i = 0; i < ncc; ++i) {
-      const int c = c0 + i;
-      const int bm = bmin_b[c];
-      const int ne = Q + bspan_b[c];
-      const int64_t sb = t0 + bm;
-      E* dst = lds + (int64_t)i * stride;
-      if constexpr (U8) {
-        const uint8_t* row = reinterpret_cast<const uint8_t*>(xv) + (int64_t)c * ld;
-        const uint32_t pv = (pad_mode == PDD_PAD_VALUE) ? (uint32_t)padvals[c] : 0u;
-        for (int e = threadIdx.x; e < ne; e += NT) {
-          E v;
+    if constexpr (DMA) {
+      int younger = 0;
 #pragma unroll
-          for (int h = 0; h < WORDS; ++h) {
-            uint32_t lo, hi;
-            const int64_t s0 = sb + e + (2 * h) * Q, s1 = s0 + Q;
-            if (pad_mode == PDD_PAD_ROTATE) {
-              lo = row[wrap_mod(s0, N)];
-              hi = row[wrap_mod(s1, N)];
-            } else {
-              lo = (s0 >= 0 && s0 < N) ? (uint32_t)row[s0] : pv;
-              hi = (s1 >= 0 && s1 < N) ? (uint32_t)row[s1] : pv;
-            }
-            set_w(v, h, lo | (hi << 16));
-          }
-          dst[e] = v;
-        }
-      } else {
-        const float* row = reinterpret_cast<const float*>(xv) + (int64_t)c * ld;
-        const float pv = (pad_mode == PDD_PAD_VALUE) ? padvals[c] : 0.f;
-        for (int e = threadIdx.x; e < ne; e += NT) {
-          E v;
-#pragma unroll
-          for (int k = 0; k < S; ++k) {
-            const int64_t s = sb + e + k * Q;
-            float f;
-            if (pad_mode == PDD_PAD_ROTATE) f = row[wrap_mod(s, N)];
-            else f = (s >= 0 && s < N) ? row[s] : pv;
-            set_w(v, k, __float_as_uint(f));
-          }
-          dst[e] = v;
-        }
-      }
+      for (int s2 = 1; s2 < NBUF - 1; ++s2) younger += pend[s2];
+      wait_vmcnt(younger);
     }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // offsets of this chunk's channels for the wave's trials, into SGPRs
+    // before any LDS read is issued (scalar loads share lgkmcnt with LDS):
+    // rel[c][d] = table[d][c] - bmin(block, c) >= 0
+    int off[CC][DPW];
+#pragma unroll
+    for (int i = 0; i < CC; ++i) {
+      const int* rp = rel + (int64_t)(c0 + (i < ncc ? i : 0)) * Dpad + d0;
+#pragma unroll
+      for (int j = 0; j < DPW; ++j) off[i][j] = rp[j];
+    }
+    {
+      // refill the buffer chunk k-1 used (every wave is past it: barrier)
+      const int cn = c0 + (NBUF - 1) * cc;
+      int b = cur + NBUF - 1;
+      b = b >= NBUF ? b - NBUF : b;
+      const int n = (cn < C && !(dbg & 1)) ? stage(cn, b) : 0;  // dbg bit 0: timing only
+#pragma unroll
+      for (int s2 = 0; s2 < NBUF - 2; ++s2) pend[s2] = pend[s2 + 1];
+      pend[NBUF - 2] = n;
+    }
     // ---- accumulate: every wave reads the image at its trials' shifts
-    for (int i = 0; i < ncc; ++i) {
-      const int c = c0 + i;
-      const int bm = bmin_b[c];
-      const int* tb = tab + (int64_t)c * Dpad + d0;
-      const E* base = lds + (int64_t)i * stride + lane;
+    const E* img = lds + cur * buf_elems;
+#pragma unroll
+    for (int i = 0; i < CC; ++i) {
+      if (i >= ncc || (dbg & 2)) break;  // dbg bit 1: timing only, staging without accumulation
+      const E* base = img + (int64_t)i * stride + lane;
 #pragma unroll
       for (int j = 0; j < DPW; ++j) {
-        const E* p = base + (tb[j] - bm);
+        const E* p = base + off[i][j];
+        E v[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) v[g] = p[g * 64];
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-          const E v = p[g * 64];
           if constexpr (U8) {
 #pragma unroll
-            for (int h = 0; h < WORDS; ++h) acc16[j][g][h] += get_w(v, h);
+            for (int h = 0; h < WORDS; ++h) acc16[j][g][h] += get_w(v[g], h);
           } else {
 #pragma unroll
-            for (int k = 0; k < S; ++k) accf[j][g][k] += __uint_as_float(get_w(v, k));
+            for (int k = 0; k < S; ++k) accf[j][g][k] += __uint_as_float(get_w(v[g], k));
           }
         }
       }
@@ -187,6 +383,7 @@ __global__ __launch_bounds__(NW * 64) void k_sweep(
         }
       }
     }
+    cur = cur + 1 == NBUF ? 0 : cur + 1;
   }
   if constexpr (U8) {
 #pragma unroll
@@ -215,22 +412,225 @@ __global__ __launch_bounds__(NW * 64) void k_sweep(
   }
 }
 
+// ------------------------------------------------------------------ linear image
+// float32 kernel with a LINEAR two-copy LDS image (the fast path):
+//   copy r (r = 0, 1) of channel c holds X(c, t0 + bmin_c + r + e), e < W.
+// A trial whose relative shift is `off` reads copy (off & 1) at the even
+// position off - (off & 1): every lane's 8-byte ds_read_b64 (2 consecutive
+// samples) is aligned and conflict-free whatever the shift.  The copies are
+// filled with 16-byte LDS-DMA (global_load_lds_dwordx4: 1 KiB of contiguous
+// samples per wave-instruction, 4x fewer staging instructions than the 4-byte
+// DMA a striped image needs).
+typedef __attribute__((address_space(3))) float lds_float_t;
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) f32x2_t lds_f32x2_t;
+
+__device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
+  return (uint32_t)(uintptr_t)(const lds_float_t*)p;
+}
+
+// 2 x ceil(need/256) DMA wave-instructions, spread over the NW waves.
+template <int NW>
+__device__ __forceinline__ int stage_lin_dma(float* dst, int W, const float* rb, int need, int w,
+                                             int lane) {
+  // need4 = need rounded up to whole 16-byte groups (the caller checked that
+  // X(sb + 1 + need4 - 1) is inside the row); groups wholly past need4
+  // re-load the last valid group into their (never read) slots
+  const int need4 = (need + 3) & ~3;
+  const int nq = (need4 + 255) >> 8;
+  const int last = need4 - 4;
+  for (int q = w; q < 2 * nq; q += NW) {
+    const int r = q >= nq ? 1 : 0;
+    const int qq = q - r * nq;
+    const int e = min(qq * 256 + lane * 4, last);
+    const float* src = rb + r + e;
+    const uint32_t la = lds_addr_of(dst + r * W + qq * 256);
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(__builtin_amdgcn_readfirstlane(la))
+        : "memory");
+  }
+  return w < 2 * nq ? (2 * nq - 1 - w) / NW + 1 : 0;
+}
+
+template <int NT>
+__device__ __forceinline__ void stage_lin_regs(float* dst, int W, const float* row, int64_t N,
+                                               int64_t sb, int need, int pad_mode, float pv) {
+  for (int e = threadIdx.x; e < need; e += NT) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int64_t s = sb + r + e;
+      float f;
+      if (pad_mode == PDD_PAD_ROTATE) f = row[wrap_mod(s, N)];
+      else f = (s >= 0 && s < N) ? row[s] : pv;
+      dst[r * W + e] = f;
+    }
+  }
+}
+
+template <int G, int DPW, int NW, int CC, int NBUF>
+__global__ __launch_bounds__(NW * 64) void k_sweep_lin(
+    const void* __restrict__ xv, int64_t ld, int C, int64_t N, const int* __restrict__ rel,
+    int Dpad, int D, const int* __restrict__ bmin, const int* __restrict__ bspan, int pad_mode,
+    const float* __restrict__ padvals, float* __restrict__ out, int64_t ld_out, int64_t n_out,
+    int dbg, int W, int n_tblk, int n_dblk) {
+  constexpr int TB = 128 * G;  // samples per tile: G groups x 64 lanes x 2
+  constexpr int DB = NW * DPW;
+  constexpr int NT = NW * 64;
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  const int chan_f = 2 * W;
+  const int buf_f = CC * chan_f;
+  const float* x = reinterpret_cast<const float*>(xv);
+
+  const int total = n_tblk * n_dblk;
+  const int full = (total / 8) * 8;
+  const int bid = blockIdx.x;
+  const int L = (bid < full) ? (bid % 8) * (total / 8) + bid / 8 : bid;
+  const int dblk = L % n_dblk, tblk = L / n_dblk;
+  const int64_t t0 = (int64_t)tblk * TB;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int d0 = dblk * DB + w * DPW;
+  const int* bmin_b = bmin + (int64_t)dblk * C;
+  const int* bspan_b = bspan + (int64_t)dblk * C;
+
+  auto stage = [&](int c0, int b) -> int {
+    const int ncc = min(CC, C - c0);
+    int ndma = 0;
+    for (int i = 0; i < ncc; ++i) {
+      const int c = c0 + i;
+      const int need = TB + bspan_b[c];
+      const int64_t sb = t0 + bmin_b[c];
+      float* dst = smf + b * buf_f + i * chan_f;
+      const float* row = x + (int64_t)c * ld;
+      if (sb >= 0 && sb + 1 + ((need + 3) & ~3) <= N) {
+        ndma += stage_lin_dma<NW>(dst, W, row + sb, need, w, lane);
+      } else {
+        const float pv = (pad_mode == PDD_PAD_VALUE) ? padvals[c] : 0.f;
+        stage_lin_regs<NT>(dst, W, row, N, sb, need, pad_mode, pv);
+      }
+    }
+    return ndma;
+  };
+
+  float acc[DPW][G][2];
+#pragma unroll
+  for (int j = 0; j < DPW; ++j)
+#pragma unroll
+    for (int g = 0; g < G; ++g) acc[j][g][0] = acc[j][g][1] = 0.f;
+
+  int pend[NBUF];
+#pragma unroll
+  for (int s2 = 0; s2 < NBUF; ++s2) pend[s2] = 0;
+#pragma unroll
+  for (int s2 = 0; s2 < NBUF - 1; ++s2)
+    if (s2 * CC < C) pend[s2] = stage(s2 * CC, s2);
+  const uint32_t lane_byte = lds_addr_of(smf) + lane * 8;
+  int cur = 0;
+  for (int c0 = 0; c0 < C; c0 += CC) {
+    const int ncc = min(CC, C - c0);
+    {
+      int younger = 0;
+#pragma unroll
+      for (int s2 = 1; s2 < NBUF - 1; ++s2) younger += pend[s2];
+      wait_vmcnt(younger);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    int off[CC][DPW];
+#pragma unroll
+    for (int i = 0; i < CC; ++i) {
+      const int* rp = rel + (int64_t)(c0 + (i < ncc ? i : 0)) * Dpad + d0;
+#pragma unroll
+      for (int j = 0; j < DPW; ++j) off[i][j] = rp[j];
+    }
+    {
+      const int cn = c0 + (NBUF - 1) * CC;
+      int b = cur + NBUF - 1;
+      b = b >= NBUF ? b - NBUF : b;
+      const int n = (cn < C && !(dbg & 1)) ? stage(cn, b) : 0;
+#pragma unroll
+      for (int s2 = 0; s2 < NBUF - 2; ++s2) pend[s2] = pend[s2 + 1];
+      pend[NBUF - 2] = n;
+    }
+#pragma unroll
+    for (int i = 0; i < CC; ++i) {
+      if (i >= ncc || (dbg & 2)) break;  // dbg bit 1: timing only
+      const uint32_t cbase = lane_byte + (uint32_t)((cur * buf_f + i * chan_f) * 4);
+#pragma unroll
+      for (int j = 0; j < DPW; ++j) {
+        const int o = off[i][j];
+        const int r = o & 1;
+        const uint32_t a0 = cbase + (uint32_t)((r * W + (o - r)) * 4);
+        f32x2_t v[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          uint32_t a = a0 + g * 512;
+          asm volatile("" : "+v"(a));  // keep 8 separate ds_read_b64 (no read2st64 merge)
+          v[g] = *(const lds_f32x2_t*)(uintptr_t)a;
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          acc[j][g][0] += v[g].x;
+          acc[j][g][1] += v[g].y;
+        }
+      }
+    }
+    cur = cur + 1 == NBUF ? 0 : cur + 1;
+  }
+#pragma unroll
+  for (int j = 0; j < DPW; ++j) {
+    const int d = d0 + j;
+    if (d >= D) continue;
+    float* orow = out + (int64_t)d * ld_out;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t t = t0 + g * 128 + 2 * lane;
+      if (t + 1 < n_out) {
+        orow[t] = acc[j][g][0];
+        orow[t + 1] = acc[j][g][1];
+      } else if (t < n_out) {
+        orow[t] = acc[j][g][0];
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ variants
 struct Variant {
   bool u8;
-  int S, G, DPW, NW;
+  int S, G, DPW, NW, CC, NBUF;
+  bool lin;  // float32 linear two-copy image (k_sweep_lin) instead of the striped one
   int elem_bytes() const { return u8 ? 2 * S : 4 * S; }
   int Q() const { return 64 * G; }
-  int TB() const { return S * 64 * G; }
+  int TB() const { return lin ? 128 * G : S * 64 * G; }
   int DB() const { return NW * DPW; }
+  // LDS "stride" argument and bytes per channel per buffer for a max span
+  int64_t stride_for(int max_span) const {
+    return lin ? (TB() + max_span + 255) / 256 * 256 : (Q() + max_span + 15) / 16 * 16;
+  }
+  int64_t chan_bytes(int64_t stride) const { return lin ? 2 * stride * 4 : stride * elem_bytes(); }
 };
 
-// Candidate tilings, best first; the plan takes the first whose LDS image of
-// one channel fits the budget.
-static const Variant kF32Variants[] = {{false, 2, 4, 8, 4}, {false, 2, 4, 2, 4}, {false, 2, 4, 1, 1}};
-static const Variant kU8Variants[] = {{true, 4, 2, 8, 4}, {true, 4, 2, 2, 4}, {true, 4, 2, 1, 1}};
+// Candidate tilings, best first; the plan takes the first whose LDS ring fits
+// the budget.
+static const Variant kF32Variants[] = {{false, 4, 4, 4, 8, 2, 2, false},
+                                       {false, 2, 8, 4, 8, 2, 3, true},
+                                       {false, 4, 4, 1, 8, 1, 2, false},
+                                       {false, 4, 1, 1, 1, 1, 2, false}};
+static const Variant kU8Variants[] = {{true, 8, 2, 4, 8, 4, 2, false},
+                                      {true, 8, 2, 4, 8, 2, 2, false},
+                                      {true, 8, 2, 1, 8, 1, 2, false},
+                                      {true, 8, 1, 1, 1, 1, 2, false}};
 
-static constexpr int kLdsBudget = 48 * 1024;   // per workgroup, 3 workgroups per CU
+static constexpr int kLdsBudget = 76 * 1024;   // per workgroup: 2 workgroups per CU
 static constexpr int kLdsMax = 160 * 1024;
 
 typedef void (*sweep_fn)(const void*, int64_t, int, int64_t, const int*, int, int, const int*,
@@ -238,17 +638,36 @@ typedef void (*sweep_fn)(const void*, int64_t, int, int64_t, const int*, int, in
                          int);
 
 static sweep_fn kernel_for(const Variant& v) {
-#define V(U, S_, G_, DPW_, NW_)                                                                 \
-  if (v.u8 == U && v.S == S_ && v.G == G_ && v.DPW == DPW_ && v.NW == NW_)                     \
-    return k_sweep<U, S_, G_, DPW_, NW_>;
-  V(false, 2, 4, 8, 4)
-  V(false, 2, 4, 2, 4)
-  V(false, 2, 4, 1, 1)
-  V(true, 4, 2, 8, 4)
-  V(true, 4, 2, 2, 4)
-  V(true, 4, 2, 1, 1)
+  if (v.lin) {
+    if (v.G == 8 && v.DPW == 4 && v.NW == 8 && v.CC == 2 && v.NBUF == 3) return k_sweep_lin<8, 4, 8, 2, 3>;
+    if (v.G == 8 && v.DPW == 4 && v.NW == 8 && v.CC == 1 && v.NBUF == 3) return k_sweep_lin<8, 4, 8, 1, 3>;
+    return nullptr;
+  }
+#define V(U, S_, G_, DPW_, NW_, CC_, NB_)                                                     \
+  if (v.u8 == U && v.S == S_ && v.G == G_ && v.DPW == DPW_ && v.NW == NW_ && v.CC == CC_ &&  \
+      v.NBUF == NB_)                                                                         \
+    return k_sweep<U, S_, G_, DPW_, NW_, CC_, NB_>;
+  V(false, 4, 4, 4, 8, 2, 2)
+  V(false, 4, 4, 1, 8, 1, 2)
+  V(false, 4, 1, 1, 1, 1, 2)
+  V(true, 8, 2, 4, 8, 4, 2)
+  V(true, 8, 2, 4, 8, 2, 2)
+  V(true, 8, 2, 1, 8, 1, 2)
+  V(true, 8, 1, 1, 1, 1, 2)
 #undef V
   return nullptr;
+}
+
+// Developer knobs (never set in production runs): PDD_SWEEP_DEBUG bit 0 makes
+// the kernel skip re-staging (timing experiments only, wrong results);
+// PDD_SWEEP_VARIANT forces a candidate tiling by index.
+static int debug_flags() {
+  const char* e = getenv("PDD_SWEEP_DEBUG");
+  return e ? atoi(e) : 0;
+}
+static int forced_variant() {
+  const char* e = getenv("PDD_SWEEP_VARIANT");
+  return e ? atoi(e) : -1;
 }
 
 }  // namespace pdd
@@ -257,7 +676,7 @@ struct pdd_sweep_plan {
   pdd::Variant v;
   int64_t D, C, Dpad, n_dblk;
   int max_span, stride, cc, lds_bytes;
-  int* d_tab = nullptr;    // [C][Dpad]
+  int* d_tab = nullptr;    // [C][Dpad] shifts relative to the block minimum
   int* d_bmin = nullptr;   // [n_dblk][C]
   int* d_bspan = nullptr;  // [n_dblk][C]
   int max_bin = 0, min_bin = 0;
@@ -274,9 +693,10 @@ int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int d
               "pdd_sweep_plan_create: bad extents D=%lld C=%lld", (long long)D, (long long)C);
   PDD_REQUIRE(dtype == PDD_F32 || dtype == PDD_U8, "pdd_sweep_plan_create: dtype must be F32 or U8");
   const Variant* cands = dtype == PDD_U8 ? kU8Variants : kF32Variants;
-  const int ncand = 3;
+  const int ncand = 4;
 
-  for (int vi = 0; vi < ncand; ++vi) {
+  const int fv = forced_variant();
+  for (int vi = (fv >= 0 && fv < ncand) ? fv : 0; vi < ncand; ++vi) {
     const Variant v = cands[vi];
     const int64_t DB = v.DB();
     const int64_t n_dblk = cdiv(D, DB);
@@ -303,18 +723,24 @@ int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int d
         mn = std::min(mn, lo);
       }
     }
-    const int64_t stride = v.Q() + max_span;
-    const int64_t per_chan = stride * v.elem_bytes();
+    // offsets relative to the block's minimum shift at each channel (what the
+    // kernel adds to its LDS base): rel[c][d] = table[d][c] - bmin[d / DB][c]
+    for (int64_t c = 0; c < C; ++c)
+      for (int64_t d = 0; d < Dpad; ++d) tab[(size_t)(c * Dpad + d)] -= bmin[(size_t)((d / DB) * C + c)];
+    // stride rounded to 16 elements: an LDS-DMA wave-instruction writes 16
+    // whole elements; NBUF chunk buffers of CC channels
+    const int64_t stride = v.stride_for(max_span);
+    const int64_t per_chan = v.NBUF * v.chan_bytes(stride);
     const bool last = (vi == ncand - 1);
-    if (per_chan > kLdsBudget && !(last && per_chan <= kLdsMax)) {
+    const int64_t need = per_chan * v.CC;
+    if (need > kLdsBudget && !(last && need <= kLdsMax)) {
       if (last) {
         set_error("pdd_sweep_plan_create: DM grid too sparse for one LDS tile (span %d bins)", max_span);
         return -1;
       }
       continue;
     }
-    int cc = (int)std::max<int64_t>(1, kLdsBudget / per_chan);
-    cc = (int)std::min<int64_t>(cc, C);
+    const int cc = v.CC;
     pdd_sweep_plan* p = new pdd_sweep_plan();
     p->v = v;
     p->D = D;
@@ -384,7 +810,7 @@ int pdd_sweep_execute(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
   PDD_REQUIRE(fn != nullptr, "pdd_sweep_execute: no kernel");
   hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(p->v.NW * 64), p->lds_bytes,
                      as_stream(stream), x, ld, (int)p->C, N, p->d_tab, (int)p->Dpad, (int)p->D,
-                     p->d_bmin, p->d_bspan, pad_mode, padvals, out, ld_out, n_out, p->cc,
+                     p->d_bmin, p->d_bspan, pad_mode, padvals, out, ld_out, n_out, debug_flags(),
                      p->stride, (int)n_tblk, (int)p->n_dblk);
   PDD_LAUNCHED();
   return 0;

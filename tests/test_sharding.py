@@ -1,0 +1,111 @@
+"""Multi-rank paths on CPU: world_size-2 (and 3) gloo process groups running
+the same partition / broadcast / gather code the GPU box runs over RCCL.
+The per-rank compute is the oracle sweep here (injected); on the GPU it is
+the HIP DMSweep."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from pypulsar_amd import sharding
+
+DT = 64e-6
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _band(C):
+    foff = -300.0 / C
+    return 1550.0 + foff / 2 + foff * np.arange(C)
+
+
+def _data(C, N):
+    rng = np.random.default_rng(3)
+    return np.clip(np.round(rng.normal(128, 16, (C, N))), 0, 255).astype(np.float32)
+
+
+def _oracle_sweep(freqs, n_out):
+    from oracle import spectra_oracle as orc
+
+    def fn(x, dms):
+        tab = orc.sweep_table(dms, freqs, DT)
+        return torch.from_numpy(orc.sweep_plane(x.numpy().astype(np.float64), tab, n_out=n_out)
+                                .astype(np.float32))
+    return fn
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        C, N = 16, 1000
+        freqs = _band(C)
+        dms = np.linspace(0.0, 40.0, 11)
+        from oracle import spectra_oracle as orc
+        n_out = N - int(orc.sweep_table(dms, freqs, DT).max())
+        x = torch.from_numpy(_data(C, N)) if rank == 0 else None
+        plane = sharding.dm_sharded_sweep(x, (C, N), torch.float32, dms, freqs, DT, n_out,
+                                          sweep_fn=_oracle_sweep(freqs, n_out), src=0, dst=0)
+        # time-block shards: each rank its own output range, no collective
+        tab = orc.sweep_table(dms, freqs, DT)
+        lo, hi, ilo, ihi = sharding.timeblock_ranges(n_out, world, tab.max())[rank]
+        xb = _data(C, N)[:, ilo:min(ihi, N)].astype(np.float64)
+        part = orc.sweep_plane(xb, tab, n_out=hi - lo)
+        parts = [None] * world
+        dist.all_gather_object(parts, part)
+        if rank == 0:
+            q.put(("dm", plane.numpy()))
+            q.put(("tb", np.concatenate(parts, axis=1)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_sweeps_equal_one_shot(world):
+    from oracle import spectra_oracle as orc
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    C, N = 16, 1000
+    freqs = _band(C)
+    dms = np.linspace(0.0, 40.0, 11)
+    tab = orc.sweep_table(dms, freqs, DT)
+    want = orc.sweep_plane(_data(C, N).astype(np.float64), tab)
+    np.testing.assert_array_equal(got["dm"].astype(np.float64), want)
+    np.testing.assert_array_equal(got["tb"], want)
+
+
+def test_dm_slices_balance():
+    s = sharding.dm_slices(10, 3)
+    assert s[0][0] == 0 and s[-1][1] == 10
+    assert all(a[1] == b[0] for a, b in zip(s, s[1:]))
+    # DDplan work weights (1/downsamp): heavier trials spread more thinly
+    w = np.r_[np.ones(100), np.full(100, 0.25)]
+    sl = sharding.dm_slices(200, 2, w)
+    assert sl[0][1] < 100
+    assert sharding.dm_slices(3, 8)[-1] == (3, 3)
+
+
+def test_timeblock_ranges_cover():
+    r = sharding.timeblock_ranges(1000, 4, 37)
+    assert r[0][0] == 0 and r[-1][1] == 1000
+    assert all(b[2] - a[2] == a[1] - a[0] for a, b in zip(r, r[1:]))
+    assert all(x[3] - x[1] == 37 for x in r)
