@@ -175,7 +175,8 @@ def main():
     uniq_bytes = C * N * s_in + len(dms) * n_out * 4
     achieved_gbs = uniq_bytes / (kern_ms * 1e-3) / 1e9
     pmc_key = "%s_%s" % (args.config, args.dtype)
-    traffic = load_pmc(os.path.join(ROOT, "profiles", "pmc_sweep.json"), pmc_key)
+    pmc = load_pmc(os.path.join(ROOT, "profiles", "pmc_sweep.json"), pmc_key)
+    traffic = pmc.get("hbm_bytes_per_launch") if isinstance(pmc, dict) else None
 
     if rank == 0:
         line = {
