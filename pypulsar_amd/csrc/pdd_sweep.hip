@@ -1021,6 +1021,390 @@ __global__ __launch_bounds__(NW * 64) void k_sweep_ring(
   }
 }
 
+// Four ds_read_b128 at a + 1024*g (g < 4) in ONE asm statement: all four are
+// in flight together and use the instruction offset field.  The results are
+// NOT ready when the statement ends; lgkm_wait1<N>(v) waits until at most N
+// LDS operations are outstanding and ties register v to that wait.
+struct Rd4 {
+  f32x4_t v[4];
+};
+__device__ __forceinline__ void ds_read4_b128(Rd4& r, uint32_t a) {
+  asm volatile(
+      "ds_read_b128 %0, %4\n\t"
+      "ds_read_b128 %1, %4 offset:1024\n\t"
+      "ds_read_b128 %2, %4 offset:2048\n\t"
+      "ds_read_b128 %3, %4 offset:3072"
+      : "=&v"(r.v[0]), "=&v"(r.v[1]), "=&v"(r.v[2]), "=&v"(r.v[3])
+      : "v"(a)
+      : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait1(f32x4_t& v) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "n"(N) : "memory");
+}
+
+// ------------------------------------------------------------------ warp-specialised
+// float32 striped kernel with DEDICATED loader waves.  Waves 0..NCW-1 only
+// read the striped image (ds_read_b128, one shift per wave and channel) and
+// add; waves NCW..NCW+NLW-1 only stage (4-byte LDS-DMA of the sample windows
+// and of the chunk's shifts).  The two roles meet at one s_barrier per chunk
+// of CC channels: before barrier k the loaders retire chunk k's DMAs with a
+// counted vmcnt (chunks k+1 .. k+NBUF-2 stay in flight); after it they refill
+// the buffer chunk k-1 used, which every compute wave has finished.
+//   meta[dblk][c] = {bmin, span};  rel[dblk][c][DB] = shift - bmin
+template <int Q, int NLW>
+__device__ __forceinline__ void stage_edge_lanes(uint4* dst, const float* row, int64_t N, int64_t sb,
+                                                 int ne, int pad_mode, float pv, int lw, int lane) {
+  for (int e = lw * 64 + lane; e < ne; e += NLW * 64) {
+    uint4 v;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t s = sb + e + k * Q;
+      float f;
+      if (pad_mode == PDD_PAD_ROTATE) f = row[wrap_mod(s, N)];
+      else f = (s >= 0 && s < N) ? row[s] : pv;
+      set_w(v, k, __float_as_uint(f));
+    }
+    dst[e] = v;
+  }
+}
+
+template <int G, int DPW, int NCW, int NLW, int CC, int NBUF>
+__global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_ws(
+    const void* __restrict__ xv, int64_t ld, int C, int64_t N, const int* __restrict__ rel,
+    int Dpad, int D, const int* __restrict__ meta, const int* __restrict__ unused, int pad_mode,
+    const float* __restrict__ padvals, float* __restrict__ out, int64_t ld_out, int64_t n_out,
+    int dbg, int stride, int n_tblk, int n_dblk) {
+  constexpr int Q = 64 * G;
+  constexpr int TB = 4 * Q;
+  constexpr int DB = NCW * DPW;
+  static_assert(CC * DB <= 64, "one metadata DMA per chunk");
+  static_assert(DPW == 4, "a wave's shifts are read as one ds_read_b128");
+  static_assert(NBUF >= 2, "ring depth");
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  uint4* img = reinterpret_cast<uint4*>(smf);
+  const int buf_e = CC * stride;                              // elements per chunk buffer
+  int* metar = reinterpret_cast<int*>(img + NBUF * buf_e);    // [NBUF][64] shifts
+  const float* x = reinterpret_cast<const float*>(xv);
+
+  const int total = n_tblk * n_dblk;
+  const int full = (total / 8) * 8;
+  const int bid = blockIdx.x;
+  const int L = (bid < full) ? (bid % 8) * (total / 8) + bid / 8 : bid;
+  const int dblk = L % n_dblk, tblk = L / n_dblk;
+  const int64_t t0 = (int64_t)tblk * TB;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int* meta_b = meta + (int64_t)dblk * C * 2;
+  const int* rel_b = rel + (int64_t)dblk * C * DB;
+  const int nchunk = (C + CC - 1) / CC;
+
+  if (w >= NCW) {
+    // ---------------- loader waves
+    const int lw = w - NCW;
+    auto issue = [&](int k) -> int {
+      const int b = k % NBUF;
+      const int c0 = k * CC;
+      const int ncc = min(CC, C - c0);
+      int n = 0;
+      if (lw == 0) {
+        dma_ints(metar + b * 64, rel_b + (int64_t)c0 * DB, ncc * DB, lane);
+        ++n;
+      }
+      for (int i = 0; i < ncc; ++i) {
+        const int c = c0 + i;
+        const int bm = meta_b[2 * c];
+        const int ne = Q + meta_b[2 * c + 1];
+        const int64_t sb = t0 + bm;
+        uint4* dst = img + (int64_t)(b * CC + i) * stride;
+        const float* row = x + (int64_t)c * ld;
+        if (sb >= 0 && sb + 3 * Q + ne <= N) {
+          if (!(dbg & 1)) n += stage_channel_dma<Q, NLW>(dst, row + sb, ne, lw, lane);
+        } else {
+          const float pv = (pad_mode == PDD_PAD_VALUE) ? padvals[c] : 0.f;
+          stage_edge_lanes<Q, NLW>(dst, row, N, sb, ne, pad_mode, pv, lw, lane);
+        }
+      }
+      return n;
+    };
+    int pend[NBUF];  // pend[s]: DMAs this wave has in flight for chunk k+s
+#pragma unroll
+    for (int s = 0; s < NBUF; ++s) pend[s] = 0;
+#pragma unroll
+    for (int s = 0; s < NBUF - 1; ++s)
+      if (s < nchunk) pend[s] = issue(s);
+    for (int k = 0; k < nchunk; ++k) {
+      int younger = 0;
+#pragma unroll
+      for (int s = 1; s < NBUF - 1; ++s) younger += pend[s];
+      wait_vmcnt(younger);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int s = 0; s < NBUF - 2; ++s) pend[s] = pend[s + 1];
+      pend[NBUF - 2] = (k + NBUF - 1 < nchunk) ? issue(k + NBUF - 1) : 0;
+    }
+    return;
+  }
+
+  // ---------------- compute waves
+  float acc[DPW][G][4];
+#pragma unroll
+  for (int j = 0; j < DPW; ++j)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) acc[j][g][k2] = 0.f;
+  const uint32_t lane_byte = lds_addr_of(img) + lane * 16;
+  const uint32_t meta_base = lds_addr_of(metar) + w * DPW * 4;
+  static_assert(G == 4, "one Rd4 batch = the 4 groups of a trial");
+  for (int k = 0; k < nchunk; ++k) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int b = k % NBUF;
+    const int ncc = min(CC, C - k * CC);
+    if (dbg & 2) continue;
+    typedef int i32x4_t __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) i32x4_t lds_i32x4_t;
+    i32x4_t o[CC];
+#pragma unroll
+    for (int i = 0; i < CC; ++i)
+      o[i] = *(const lds_i32x4_t*)(uintptr_t)(meta_base + (uint32_t)((b * 64 + i * DB) * 4));
+#pragma unroll
+    for (int i = 0; i < CC; ++i) {
+      if (i >= ncc) break;
+      const uint32_t cb = lane_byte + (uint32_t)((b * CC + i) * stride * 16);
+      const int ov[4] = {o[i].x, o[i].y, o[i].z, o[i].w};
+#pragma unroll
+      for (int j = 0; j < DPW; ++j) {
+        Rd4 r;
+        ds_read4_b128(r, cb + (uint32_t)(ov[j] * 16));
+        lgkm_wait1<3>(r.v[0]);
+        acc[j][0][0] += r.v[0].x; acc[j][0][1] += r.v[0].y;
+        acc[j][0][2] += r.v[0].z; acc[j][0][3] += r.v[0].w;
+        lgkm_wait1<2>(r.v[1]);
+        acc[j][1][0] += r.v[1].x; acc[j][1][1] += r.v[1].y;
+        acc[j][1][2] += r.v[1].z; acc[j][1][3] += r.v[1].w;
+        lgkm_wait1<1>(r.v[2]);
+        acc[j][2][0] += r.v[2].x; acc[j][2][1] += r.v[2].y;
+        acc[j][2][2] += r.v[2].z; acc[j][2][3] += r.v[2].w;
+        lgkm_wait1<0>(r.v[3]);
+        acc[j][3][0] += r.v[3].x; acc[j][3][1] += r.v[3].y;
+        acc[j][3][2] += r.v[3].z; acc[j][3][3] += r.v[3].w;
+      }
+    }
+  }
+  const int d0 = dblk * DB + w * DPW;
+#pragma unroll
+  for (int j = 0; j < DPW; ++j) {
+    const int d = d0 + j;
+    if (d >= D) continue;
+    float* orow = out + (int64_t)d * ld_out;
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2)
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int64_t t = t0 + k2 * Q + g * 64 + lane;
+        if (t < n_out) orow[t] = acc[j][g][k2];
+      }
+  }
+}
+
+// ------------------------------------------------------------------ interleaved
+// The production sweep.  A pre-pass (k_interleave) rewrites each channel of
+// the input segment as 16-byte ELEMENTS that hold 4 samples a quarter of the
+// segment apart:
+//     R[c][j] = ( X(c, b+j), X(c, b+j+Qs), X(c, b+j+2Qs), X(c, b+j+3Qs) ),
+//     b = t_base + lo,  j < nR = Qs + hi - lo + 64
+// with the reference pad semantics (value / rotate) baked in, so the sweep
+// never sees an edge.  It is a pure re-layout (each sample is read once and
+// written once, ~1x the input bytes; u8/f32 input both become float32).
+// A sweep tile (DB trials x Tq elements) then stages each channel's window
+// R[c][t0 + bmin_c - lo + e], e < Tq + span_c, with 1 KiB LDS-DMA
+// instructions (global_load_lds_dwordx4, one element per lane) issued by
+// dedicated loader waves, and every compute-wave ds_read_b128 at a trial's
+// (wave-uniform) shift returns 4 samples -- one per quarter -- that share it.
+// Output (trial d, element e, quarter k) is plane[d][t_base + e + k*Qs].
+template <typename InT>
+__global__ __launch_bounds__(256) void k_interleave(const InT* __restrict__ x, int64_t ld, int64_t N,
+                                                    int64_t base, int64_t Qs, int64_t nR,
+                                                    int pad_mode, const float* __restrict__ padvals,
+                                                    float4* __restrict__ R) {
+  const int c = blockIdx.y;
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= nR) return;
+  const InT* row = x + (int64_t)c * ld;
+  const float pv = (pad_mode == PDD_PAD_VALUE) ? padvals[c] : 0.f;
+  float v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t s = base + j + k * Qs;
+    if (s >= 0 && s < N) v[k] = (float)row[s];
+    else if (pad_mode == PDD_PAD_ROTATE) v[k] = (float)row[wrap_mod(s, N)];
+    else v[k] = pv;
+  }
+  R[(int64_t)c * nR + j] = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// n DMAs of 64 elements (1 KiB) each, q = first, first + step, ...
+__device__ __forceinline__ int stage_il_dma(uint32_t lds_dst, const float4* src, int ne, int first,
+                                            int step, int lane) {
+  const int nq = (ne + 63) >> 6;
+  for (int q = first; q < nq; q += step) {
+    const float4* s = src + q * 64 + lane;
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(s), "s"(__builtin_amdgcn_readfirstlane(lds_dst + q * 1024))
+        : "memory");
+  }
+  return first < nq ? (nq - 1 - first) / step + 1 : 0;
+}
+
+template <int G, int DPW, int NCW, int NLW, int CC, int NBUF>
+__global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
+    const float4* __restrict__ R, int64_t nR, int C, int lo, const int* __restrict__ rel,
+    const int* __restrict__ meta, float* __restrict__ out, int64_t ld_out, int D, int64_t Qs,
+    int64_t t_base, int64_t n_out, int stride, int n_tblk, int n_dblk, int dbg) {
+  constexpr int Tq = 64 * G;
+  constexpr int DB = NCW * DPW;
+  static_assert(CC * DB <= 64, "one metadata DMA per chunk");
+  static_assert(DPW == 4 && G == 4, "b128 shift reads; one Rd4 batch per trial");
+  static_assert(NBUF >= 2, "ring depth");
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  uint4* img = reinterpret_cast<uint4*>(smf);
+  const int buf_e = CC * stride;
+  int* metar = reinterpret_cast<int*>(img + NBUF * buf_e);  // [NBUF][64] shifts
+
+  // XCD-aware order: the n_dblk trial blocks of one time tile run back to
+  // back on one XCD (blocks b and b+8 share an XCD) and share its L2.
+  const int total = n_tblk * n_dblk;
+  const int full = (total / 8) * 8;
+  const int bid = blockIdx.x;
+  const int L = (bid < full) ? (bid % 8) * (total / 8) + bid / 8 : bid;
+  const int dblk = L % n_dblk, tblk = L / n_dblk;
+  const int64_t t0 = (int64_t)tblk * Tq;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int* meta_b = meta + (int64_t)dblk * C * 2;
+  const int* rel_b = rel + (int64_t)dblk * C * DB;
+  const int nchunk = (C + CC - 1) / CC;
+
+  if (w >= NCW) {
+    // ---------------- loader waves: sample windows + the chunk's shifts
+    const int lw = w - NCW;
+    const uint32_t img_lds = lds_addr_of(img);
+    auto issue = [&](int k) -> int {
+      const int b = k % NBUF;
+      const int c0 = k * CC;
+      const int ncc = min(CC, C - c0);
+      int n = 0;
+      if (lw == 0) {
+        dma_ints(metar + b * 64, rel_b + (int64_t)c0 * DB, ncc * DB, lane);
+        ++n;
+      }
+      if (!(dbg & 1)) {
+        // the chunk's channels are one DMA sequence, split over the loaders
+#pragma unroll
+        for (int i = 0; i < CC; ++i) {
+          if (i >= ncc) break;
+          const int c = c0 + i;
+          const int64_t j0 = t0 + meta_b[2 * c] - lo;
+          const int ne = Tq + meta_b[2 * c + 1];
+          n += stage_il_dma(img_lds + (uint32_t)((b * CC + i) * stride * 16), R + (int64_t)c * nR + j0,
+                            ne, lw, NLW, lane);
+        }
+      }
+      return n;
+    };
+    int pend[NBUF];  // pend[s]: DMAs this wave has in flight for chunk k+s
+#pragma unroll
+    for (int s = 0; s < NBUF; ++s) pend[s] = 0;
+#pragma unroll
+    for (int s = 0; s < NBUF - 1; ++s)
+      if (s < nchunk) pend[s] = issue(s);
+    for (int k = 0; k < nchunk; ++k) {
+      int younger = 0;
+#pragma unroll
+      for (int s = 1; s < NBUF - 1; ++s) younger += pend[s];
+      wait_vmcnt(younger);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int s = 0; s < NBUF - 2; ++s) pend[s] = pend[s + 1];
+      pend[NBUF - 2] = (k + NBUF - 1 < nchunk) ? issue(k + NBUF - 1) : 0;
+    }
+    return;
+  }
+
+  // ---------------- compute waves: ds_read_b128 at the trial's shift + adds
+  float acc[DPW][G][4];
+#pragma unroll
+  for (int j = 0; j < DPW; ++j)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) acc[j][g][k2] = 0.f;
+  const uint32_t lane_byte = lds_addr_of(img) + lane * 16;
+  const uint32_t meta_base = lds_addr_of(metar) + w * DPW * 4;
+  typedef int i32x4_t __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) i32x4_t lds_i32x4_t;
+  for (int k = 0; k < nchunk; ++k) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int b = k % NBUF;
+    const int ncc = min(CC, C - k * CC);
+    if (dbg & 2) continue;
+    i32x4_t o[CC];
+#pragma unroll
+    for (int i = 0; i < CC; ++i)
+      o[i] = *(const lds_i32x4_t*)(uintptr_t)(meta_base + (uint32_t)((b * 64 + i * DB) * 4));
+#pragma unroll
+    for (int i = 0; i < CC; ++i) {
+      if (i >= ncc) break;
+      const uint32_t cb = lane_byte + (uint32_t)((b * CC + i) * stride * 16);
+      const int ov[4] = {o[i].x, o[i].y, o[i].z, o[i].w};
+#pragma unroll
+      for (int j = 0; j < DPW; ++j) {
+        Rd4 r;
+        ds_read4_b128(r, cb + (uint32_t)(ov[j] * 16));
+        lgkm_wait1<3>(r.v[0]);
+        acc[j][0][0] += r.v[0].x; acc[j][0][1] += r.v[0].y;
+        acc[j][0][2] += r.v[0].z; acc[j][0][3] += r.v[0].w;
+        lgkm_wait1<2>(r.v[1]);
+        acc[j][1][0] += r.v[1].x; acc[j][1][1] += r.v[1].y;
+        acc[j][1][2] += r.v[1].z; acc[j][1][3] += r.v[1].w;
+        lgkm_wait1<1>(r.v[2]);
+        acc[j][2][0] += r.v[2].x; acc[j][2][1] += r.v[2].y;
+        acc[j][2][2] += r.v[2].z; acc[j][2][3] += r.v[2].w;
+        lgkm_wait1<0>(r.v[3]);
+        acc[j][3][0] += r.v[3].x; acc[j][3][1] += r.v[3].y;
+        acc[j][3][2] += r.v[3].z; acc[j][3][3] += r.v[3].w;
+      }
+    }
+  }
+  const int d0 = dblk * DB + w * DPW;
+#pragma unroll
+  for (int j = 0; j < DPW; ++j) {
+    const int d = d0 + j;
+    if (d >= D) continue;
+    float* orow = out + (int64_t)d * ld_out + t_base;
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2)
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int64_t t = t0 + g * 64 + lane;
+        if (t < Qs && t_base + t + k2 * Qs < n_out) orow[t + k2 * Qs] = acc[j][g][k2];
+      }
+  }
+}
+
 // Host: pack each DM block's channel windows (16-element granules, the DMA
 // unit) into a ring of R elements in channel order; returns the largest
 // prefetch distance P <= PMAX such that no P+1 consecutive channels overlap,
@@ -1060,12 +1444,16 @@ struct Variant {
   int S, G, DPW, NW, CC, NBUF;
   bool lin;  // float32 linear two-copy image (k_sweep_lin) instead of the striped one
   int ring;  // 1: k_sweep_ring (per-channel steps, exact-size LDS ring, deep prefetch)
+  int ws;    // > 0: k_sweep_ws with this many dedicated loader waves (NW = compute waves)
+  int il;    // 1: interleaved production path (k_interleave + k_sweep_il, ws loader waves)
+  int threads() const { return (NW + ws) * 64; }
   int elem_bytes() const { return u8 ? 2 * S : 4 * S; }
   int Q() const { return 64 * G; }
   int TB() const { return lin && S == 2 ? 128 * G : S * 64 * G; }
   int DB() const { return NW * DPW; }
   // LDS "stride" argument and bytes per channel per buffer for a max span
   int64_t stride_for(int max_span) const {
+    if (il) return (64 * G + max_span + 63) / 64 * 64;  // whole 64-element DMA granules
     return lin && S == 2 ? (TB() + max_span + 255) / 256 * 256 : (Q() + max_span + 15) / 16 * 16;
   }
   int64_t chan_bytes(int64_t stride) const {
@@ -1075,13 +1463,17 @@ struct Variant {
 
 // Candidate tilings, best first; the plan takes the first whose LDS ring fits
 // the budget.
-static const Variant kF32Variants[] = {{false, 4, 4, 4, 8, 2, 2, false, 0},
+static const Variant kF32Variants[] = {{false, 4, 4, 4, 8, 2, 3, false, 0, 2, 1},
+                                       {false, 4, 4, 4, 8, 2, 3, false, 0, 1},
+                                       {false, 4, 4, 4, 8, 2, 3, false, 0, 2},
+                                       {false, 4, 4, 4, 8, 2, 2, false, 0},
                                        {false, 4, 4, 4, 8, 1, 0, false, 1},
                                        {false, 2, 8, 4, 8, 2, 3, true, 0},
                                        {false, 4, 4, 4, 8, 2, 3, true, 0},
                                        {false, 4, 4, 1, 8, 1, 2, false, 0},
                                        {false, 4, 1, 1, 1, 1, 2, false, 0}};
-static const Variant kU8Variants[] = {{true, 8, 2, 4, 8, 4, 2, false},
+static const Variant kU8Variants[] = {{false, 4, 4, 4, 8, 2, 3, false, 0, 2, 1},
+                                      {true, 8, 2, 4, 8, 4, 2, false},
                                       {true, 8, 2, 4, 8, 2, 2, false},
                                       {true, 8, 2, 1, 8, 1, 2, false},
                                       {true, 8, 1, 1, 1, 1, 2, false}};
@@ -1095,6 +1487,13 @@ typedef void (*sweep_fn)(const void*, int64_t, int, int64_t, const int*, int, in
                          int);
 
 static sweep_fn kernel_for(const Variant& v) {
+  if (v.ws) {
+    if (!v.u8 && v.S == 4 && v.G == 4 && v.DPW == 4 && v.NW == 8 && v.CC == 2 && v.NBUF == 3 && v.ws == 1)
+      return k_sweep_ws<4, 4, 8, 1, 2, 3>;
+    if (!v.u8 && v.S == 4 && v.G == 4 && v.DPW == 4 && v.NW == 8 && v.CC == 2 && v.NBUF == 3 && v.ws == 2)
+      return k_sweep_ws<4, 4, 8, 2, 2, 3>;
+    return nullptr;
+  }
   if (v.lin && v.S == 4) {
     if (v.G == 4 && v.DPW == 4 && v.NW == 8 && v.CC == 2 && v.NBUF == 3) return k_sweep_str<4, 4, 8, 2, 3>;
     return nullptr;
@@ -1142,9 +1541,60 @@ struct pdd_sweep_plan {
   int* d_bspan = nullptr;  // [n_dblk][C]
   int max_bin = 0, min_bin = 0;
   int P = 0;               // ring kernel: prefetch distance (channels)
+  int dtype = PDD_F32;     // input element type
 };
 
 using namespace pdd;
+
+// Interleaved path: the output is produced in time segments whose
+// interleaved copy R fits a scratch budget (stream-ordered allocation, freed
+// after the segment loop); each segment is one k_interleave + one k_sweep_il.
+static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t ld, int pad_mode,
+                      const float* padvals, float* out, int64_t ld_out, int64_t n_out,
+                      void* stream) {
+  constexpr int Tq = 256;
+  const int64_t C = p->C;
+  const int64_t lo = std::min(0, p->min_bin), hi = std::max(0, p->max_bin);
+  int64_t budget = (int64_t)8 << 30;  // bytes of R per segment
+  if (const char* e = getenv("PDD_SWEEP_SEG_BYTES")) budget = std::max<int64_t>(atoll(e), 1 << 16);
+  const int64_t nr_max = budget / (C * 16);
+  int64_t seg = (nr_max - (hi - lo) - 64) / Tq * Tq * 4;  // output samples per segment
+  PDD_REQUIRE(seg > 0, "pdd_sweep_execute: delay span %lld too wide for the segment budget",
+              (long long)(hi - lo));
+  seg = std::min(seg, cdiv(n_out, 4 * Tq) * 4 * Tq);
+  const int64_t qs_max = seg / 4;
+  const int64_t nr_alloc = qs_max + (hi - lo) + 64;
+  float4* R = nullptr;
+  hipStream_t st = as_stream(stream);
+  PDD_HIP(hipMallocAsync((void**)&R, (size_t)(C * nr_alloc) * sizeof(float4), st));
+  const int dbg = debug_flags();
+  int rc = 0;
+  for (int64_t t_base = 0; t_base < n_out && rc == 0; t_base += seg) {
+    const int64_t cnt = std::min(seg, n_out - t_base);
+    const int64_t Qs = cdiv(cdiv(cnt, 4), Tq) * Tq;
+    const int64_t nR = Qs + (hi - lo) + 64;
+    dim3 g1((unsigned)cdiv(nR, 256), (unsigned)C);
+    if (p->dtype == PDD_U8)
+      hipLaunchKernelGGL(k_interleave<uint8_t>, g1, dim3(256), 0, st, (const uint8_t*)x, ld, N,
+                         t_base + lo, Qs, nR, pad_mode, padvals, R);
+    else
+      hipLaunchKernelGGL(k_interleave<float>, g1, dim3(256), 0, st, (const float*)x, ld, N,
+                         t_base + lo, Qs, nR, pad_mode, padvals, R);
+    if (hipGetLastError() != hipSuccess) { rc = -3; break; }
+    const int64_t n_tblk = Qs / Tq;
+    const int64_t blocks = n_tblk * p->n_dblk;
+    if (blocks >= (1ll << 31)) { rc = -1; break; }
+    hipLaunchKernelGGL((k_sweep_il<4, 4, 8, 2, 2, 3>), dim3((unsigned)blocks), dim3(p->v.threads()),
+                       p->lds_bytes, st, R, nR, (int)C, (int)lo, p->d_tab, p->d_bmin, out, ld_out,
+                       (int)p->D, Qs, t_base, t_base + cnt, p->stride, (int)n_tblk,
+                       (int)p->n_dblk, dbg);
+    if (hipGetLastError() != hipSuccess) rc = -3;
+  }
+  (void)hipFreeAsync(R, st);
+  if (rc == -1) set_error("pdd_sweep_execute: grid too large");
+  if (rc == -3) set_error("pdd_sweep_execute: kernel launch failed");
+  return rc;
+}
 
 extern "C" {
 
@@ -1155,7 +1605,7 @@ int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int d
               "pdd_sweep_plan_create: bad extents D=%lld C=%lld", (long long)D, (long long)C);
   PDD_REQUIRE(dtype == PDD_F32 || dtype == PDD_U8, "pdd_sweep_plan_create: dtype must be F32 or U8");
   const Variant* cands = dtype == PDD_U8 ? kU8Variants : kF32Variants;
-  const int ncand = dtype == PDD_U8 ? 4 : 6;
+  const int ncand = dtype == PDD_U8 ? 5 : 9;
 
   const int fv = forced_variant();
   for (int vi = (fv >= 0 && fv < ncand) ? fv : 0; vi < ncand; ++vi) {
@@ -1219,7 +1669,9 @@ int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int d
     const bool last = (vi == ncand - 1);
     // linear kernel: metadata rings (NBUF x 64 ints x 2) after the buffers
     const int64_t need = v.ring ? lds_budget(v)
-                                : per_chan * v.CC + (v.lin ? 2 * v.NBUF * 64 * 4 : 0);
+                                : per_chan * v.CC + (v.lin ? 2 * v.NBUF * 64 * 4 : 0) +
+                                      (v.ws ? v.NBUF * 64 * 4 : 0);
+    if (v.il && (int64_t)max_span + 64 * v.G > (int64_t)1 << 20) continue;  // windows too wide
     if (need > lds_budget(v) && !(last && need <= kLdsMax)) {
       if (last) {
         set_error("pdd_sweep_plan_create: DM grid too sparse for one LDS tile (span %d bins)", max_span);
@@ -1239,7 +1691,8 @@ int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int d
     p->cc = cc;
     p->lds_bytes = (int)need;
     p->P = ringP;
-    if (v.lin) {
+    p->dtype = dtype;
+    if (v.lin || v.ws) {
       // block-major layouts read by per-chunk metadata DMAs:
       //   rel [dblk][c][DB], meta[dblk][c] = {bmin, span}
       std::vector<int> relb((size_t)(n_dblk * C * DB));
@@ -1269,7 +1722,9 @@ int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int d
       return -2;
     }
     if (p->lds_bytes > 64 * 1024) {
-      const void* kf = v.ring ? (const void*)k_sweep_ring<4, 4, 8> : (const void*)kernel_for(v);
+      const void* kf = v.ring ? (const void*)k_sweep_ring<4, 4, 8>
+                              : v.il ? (const void*)k_sweep_il<4, 4, 8, 2, 2, 3>
+                                     : (const void*)kernel_for(v);
       e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, p->lds_bytes);
       if (e != hipSuccess) {
         set_error("pdd_sweep_plan_create: hipFuncSetAttribute: %s", hipGetErrorString(e));
@@ -1305,6 +1760,7 @@ int pdd_sweep_execute(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
   PDD_REQUIRE(pad_mode == PDD_PAD_ROTATE || (pad_mode == PDD_PAD_VALUE && padvals),
               "pdd_sweep_execute: bad pad mode %d", pad_mode);
   if (n_out == 0) return 0;
+  if (p->v.il) return execute_il(p, x, N, ld, pad_mode, padvals, out, ld_out, n_out, stream);
   // every staged index must stay inside int64 / the LDS image: the shifts are
   // bounded by the plan, the samples by N + n_out.
   const int64_t n_tblk = cdiv(n_out, p->v.TB());
@@ -1322,7 +1778,7 @@ int pdd_sweep_execute(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
   }
   sweep_fn fn = kernel_for(p->v);
   PDD_REQUIRE(fn != nullptr, "pdd_sweep_execute: no kernel");
-  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(p->v.NW * 64), p->lds_bytes,
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(p->v.threads()), p->lds_bytes,
                      as_stream(stream), x, ld, (int)p->C, N, p->d_tab, (int)p->Dpad, (int)p->D,
                      p->d_bmin, p->d_bspan, pad_mode, padvals, out, ld_out, n_out, debug_flags(),
                      p->stride, (int)n_tblk, (int)p->n_dblk);
