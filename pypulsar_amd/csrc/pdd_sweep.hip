@@ -1267,78 +1267,130 @@ __device__ __forceinline__ int stage_il_dma(uint32_t lds_dst, const float4* src,
   return first < nq ? (nq - 1 - first) / step + 1 : 0;
 }
 
+// Synchronisation of k_sweep_il: one s_barrier per chunk.  Before barrier k
+// the loader waves retire chunk k's DMAs with a counted vmcnt (chunks k+1 ..
+// k+NBUF-2 stay in flight); after it they refill the buffer chunk k-1 used.
+// (An LDS-counter variant without barriers -- loaders publish landed[b],
+// compute waves publish done[b] -- measured slower: the sweep is bound by the
+// L2/MALL->LDS staging rate, ~80 CU-cycles per 1 KiB DMA, not by the barrier.)
+//
+// Metadata: mt[dblk][c][ROW], ROW = DB + 4: the tile's DB shifts at channel c
+// relative to their minimum bmin, then {bmin, span, 0, 0}.  Every loader wave
+// DMAs the rows of chunk k into its own ring (slot k % MR) MA = NBUF chunks
+// (MA = 2(NBUF-1)) ahead, so they have landed (its own counted vmcnt) before
+// it reads the window bounds; the compute waves read the shifts from loader
+// 0's ring once the
+// chunk's barrier has passed.
+__host__ __device__ constexpr int il_ma(int nbuf) { return 2 * nbuf - 2; }
+__host__ __device__ constexpr int il_mr(int nbuf) { return nbuf <= 4 ? 8 : (nbuf <= 8 ? 16 : 32); }
+__host__ __device__ constexpr int il_slot(int cc, int db) { return (cc * (db + 4) + 63) / 64 * 64; }
+__host__ __device__ constexpr int il_meta_bytes(int nlw, int nbuf, int cc, int db) {
+  return nlw * il_mr(nbuf) * il_slot(cc, db) * 4;
+}
+
 template <int G, int DPW, int NCW, int NLW, int CC, int NBUF>
 __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
-    const float4* __restrict__ R, int64_t nR, int C, int lo, const int* __restrict__ rel,
-    const int* __restrict__ meta, float* __restrict__ out, int64_t ld_out, int D, int64_t Qs,
-    int64_t t_base, int64_t n_out, int stride, int n_tblk, int n_dblk, int dbg) {
+    const float4* __restrict__ R, int64_t nR, int C, int lo, const int* __restrict__ mt,
+    float* __restrict__ out, int64_t ld_out, int D, int64_t Qs, int64_t t_base, int64_t n_out,
+    int stride, int n_tblk, int n_dblk, int dbg) {
   constexpr int Tq = 64 * G;
   constexpr int DB = NCW * DPW;
-  static_assert(CC * DB <= 64, "one metadata DMA per chunk");
-  static_assert(DPW == 4 && G == 4, "b128 shift reads; one Rd4 batch per trial");
-  static_assert(NBUF >= 2, "ring depth");
+  constexpr int ROW = DB + 4;
+  constexpr int SLOT = il_slot(CC, DB);
+  constexpr int MA = il_ma(NBUF), MR = il_mr(NBUF);
+  static_assert(DPW == 4 && G == 4, "b128 shift reads; one trial = 4 groups");
+  static_assert(NBUF >= 2 && MA >= 2 * NBUF - 2 && MR > MA, "ring geometry");
   extern __shared__ __attribute__((aligned(16))) float smf[];
   uint4* img = reinterpret_cast<uint4*>(smf);
   const int buf_e = CC * stride;
-  int* metar = reinterpret_cast<int*>(img + NBUF * buf_e);  // [NBUF][64] shifts
+  int* metar = reinterpret_cast<int*>(img + NBUF * buf_e);  // [NLW][MR][SLOT]
 
   // XCD-aware order: the n_dblk trial blocks of one time tile run back to
   // back on one XCD (blocks b and b+8 share an XCD) and share its L2.
+  // dbg bit 4: chip-wide time-major order instead.
   const int total = n_tblk * n_dblk;
   const int full = (total / 8) * 8;
   const int bid = blockIdx.x;
-  const int L = (bid < full) ? (bid % 8) * (total / 8) + bid / 8 : bid;
+  const int L = ((dbg & 16) || bid >= full) ? bid : (bid % 8) * (total / 8) + bid / 8;
   const int dblk = L % n_dblk, tblk = L / n_dblk;
   const int64_t t0 = (int64_t)tblk * Tq;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int* meta_b = meta + (int64_t)dblk * C * 2;
-  const int* rel_b = rel + (int64_t)dblk * C * DB;
+  const int* mt_b = mt + (int64_t)dblk * C * ROW;
   const int nchunk = (C + CC - 1) / CC;
+  const bool stamps = (dbg & 4) != 0;  // dbg bit 2: per-wave cycle stamps into `out`
 
   if (w >= NCW) {
-    // ---------------- loader waves: sample windows + the chunk's shifts
+    // ---------------- loader waves: metadata rows + sample windows
+    // Top issue priority: a loader shares its SIMD with compute waves that
+    // have an LDS read or add ready every cycle.
+    if (!(dbg & 8)) __builtin_amdgcn_s_setprio(3);
     const int lw = w - NCW;
     const uint32_t img_lds = lds_addr_of(img);
-    auto issue = [&](int k) -> int {
-      const int b = k % NBUF;
-      const int c0 = k * CC;
-      const int ncc = min(CC, C - c0);
+    int* ring = metar + lw * MR * SLOT;
+    auto issue_meta = [&](int k) -> int {
+      if (k >= nchunk) return 0;
+      const int n_int = min(CC, C - k * CC) * ROW;
       int n = 0;
-      if (lw == 0) {
-        dma_ints(metar + b * 64, rel_b + (int64_t)c0 * DB, ncc * DB, lane);
-        ++n;
-      }
-      if (!(dbg & 1)) {
-        // the chunk's channels are one DMA sequence, split over the loaders
 #pragma unroll
-        for (int i = 0; i < CC; ++i) {
-          if (i >= ncc) break;
-          const int c = c0 + i;
-          const int64_t j0 = t0 + meta_b[2 * c] - lo;
-          const int ne = Tq + meta_b[2 * c + 1];
-          n += stage_il_dma(img_lds + (uint32_t)((b * CC + i) * stride * 16), R + (int64_t)c * nR + j0,
-                            ne, lw, NLW, lane);
-        }
+      for (int m = 0; m < SLOT / 64; ++m) {
+        if (m * 64 >= n_int) break;
+        dma_ints(ring + (k % MR) * SLOT + m * 64, mt_b + (int64_t)k * CC * ROW + m * 64,
+                 n_int - m * 64, lane);
+        ++n;
       }
       return n;
     };
-    int pend[NBUF];  // pend[s]: DMAs this wave has in flight for chunk k+s
+    auto issue_samples = [&](int k) -> int {
+      if (dbg & 1) return 0;
+      const int b = k % NBUF;
+      const int* ms = ring + (k % MR) * SLOT;
+      const int ncc = min(CC, C - k * CC);
+      int n = 0;
 #pragma unroll
-    for (int s = 0; s < NBUF; ++s) pend[s] = 0;
+      for (int i = 0; i < CC; ++i) {
+        if (i >= ncc) break;
+        const int bm = __builtin_amdgcn_readfirstlane(ms[i * ROW + DB]);
+        const int ne = Tq + __builtin_amdgcn_readfirstlane(ms[i * ROW + DB + 1]);
+        n += stage_il_dma(img_lds + (uint32_t)((b * CC + i) * stride * 16),
+                          R + (int64_t)(k * CC + i) * nR + (t0 + bm - lo), ne, lw, NLW, lane);
+      }
+      return n;
+    };
+    for (int k = 0; k < MA; ++k) issue_meta(k);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // prologue: every ring's first MA slots landed
+    asm volatile("" ::: "memory");
+    int hist[NBUF];  // hist[i]: DMAs this wave issued i+1 iterations ago
 #pragma unroll
-    for (int s = 0; s < NBUF - 1; ++s)
-      if (s < nchunk) pend[s] = issue(s);
+    for (int i = 0; i < NBUF; ++i) hist[i] = 0;
+#pragma unroll
+    for (int s2 = 0; s2 < NBUF - 1; ++s2) {
+#pragma unroll
+      for (int i = NBUF - 1; i > 0; --i) hist[i] = hist[i - 1];
+      hist[0] = s2 < nchunk ? issue_samples(s2) : 0;
+    }
+    uint64_t ts_poll = 0, ts_issue = 0, ts_wait = 0, tA = 0, tB = 0;
     for (int k = 0; k < nchunk; ++k) {
+      // retire chunk k (and everything older); the NBUF-2 younger chunks stay in flight
+      if (stamps) tA = __builtin_amdgcn_s_memtime();
       int younger = 0;
 #pragma unroll
-      for (int s = 1; s < NBUF - 1; ++s) younger += pend[s];
+      for (int i = 0; i < NBUF - 2; ++i) younger += hist[i];
       wait_vmcnt(younger);
+      if (stamps) { tB = __builtin_amdgcn_s_memtime(); ts_wait += tB - tA; tA = tB; }
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      if (stamps) { tB = __builtin_amdgcn_s_memtime(); ts_poll += tB - tA; tA = tB; }
+      const int n = issue_meta(k + MA) + (k + NBUF - 1 < nchunk ? issue_samples(k + NBUF - 1) : 0);
 #pragma unroll
-      for (int s = 0; s < NBUF - 2; ++s) pend[s] = pend[s + 1];
-      pend[NBUF - 2] = (k + NBUF - 1 < nchunk) ? issue(k + NBUF - 1) : 0;
+      for (int i = NBUF - 1; i > 0; --i) hist[i] = hist[i - 1];
+      hist[0] = n;
+      if (stamps) ts_issue += __builtin_amdgcn_s_memtime() - tA;
+    }
+    if (stamps && lane == 0) {
+      float* o = out + ((int64_t)blockIdx.x * (NCW + NLW) + w) * 4;
+      o[0] = (float)ts_wait; o[1] = (float)ts_poll; o[2] = (float)ts_issue; o[3] = 0.f;
     }
     return;
   }
@@ -1352,42 +1404,64 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
 #pragma unroll
       for (int k2 = 0; k2 < 4; ++k2) acc[j][g][k2] = 0.f;
   const uint32_t lane_byte = lds_addr_of(img) + lane * 16;
-  const uint32_t meta_base = lds_addr_of(metar) + w * DPW * 4;
+  const uint32_t meta_base = lds_addr_of(metar) + w * DPW * 4;  // loader 0's ring
   typedef int i32x4_t __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(3))) i32x4_t lds_i32x4_t;
+  uint64_t ts_poll = 0, ts_comp = 0, tA = 0, tB = 0;
+  __builtin_amdgcn_s_barrier();  // prologue barrier (metadata landed)
+  asm volatile("" ::: "memory");
+  if (stamps) tB = __builtin_amdgcn_s_memtime();
   for (int k = 0; k < nchunk; ++k) {
+    const int b = k % NBUF;
+    if (stamps) {
+      tA = __builtin_amdgcn_s_memtime();
+      ts_comp += tA - tB;
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    const int b = k % NBUF;
+    if (stamps) { tB = __builtin_amdgcn_s_memtime(); ts_poll += tB - tA; }
+    const int slot = k % MR;
     const int ncc = min(CC, C - k * CC);
-    if (dbg & 2) continue;
-    i32x4_t o[CC];
+    if (!(dbg & 2)) {
 #pragma unroll
-    for (int i = 0; i < CC; ++i)
-      o[i] = *(const lds_i32x4_t*)(uintptr_t)(meta_base + (uint32_t)((b * 64 + i * DB) * 4));
+      for (int i = 0; i < CC; ++i) {
+        if (i >= ncc) break;
+        const i32x4_t o =
+            *(const lds_i32x4_t*)(uintptr_t)(meta_base + (uint32_t)((slot * SLOT + i * ROW) * 4));
+        const uint32_t cb = lane_byte + (uint32_t)((b * CC + i) * stride * 16);
+        const int ov[4] = {o.x, o.y, o.z, o.w};
+        f32x4_t v[DPW][G];
 #pragma unroll
-    for (int i = 0; i < CC; ++i) {
-      if (i >= ncc) break;
-      const uint32_t cb = lane_byte + (uint32_t)((b * CC + i) * stride * 16);
-      const int ov[4] = {o[i].x, o[i].y, o[i].z, o[i].w};
+        for (int j = 0; j < DPW; ++j)
 #pragma unroll
-      for (int j = 0; j < DPW; ++j) {
-        Rd4 r;
-        ds_read4_b128(r, cb + (uint32_t)(ov[j] * 16));
-        lgkm_wait1<3>(r.v[0]);
-        acc[j][0][0] += r.v[0].x; acc[j][0][1] += r.v[0].y;
-        acc[j][0][2] += r.v[0].z; acc[j][0][3] += r.v[0].w;
-        lgkm_wait1<2>(r.v[1]);
-        acc[j][1][0] += r.v[1].x; acc[j][1][1] += r.v[1].y;
-        acc[j][1][2] += r.v[1].z; acc[j][1][3] += r.v[1].w;
-        lgkm_wait1<1>(r.v[2]);
-        acc[j][2][0] += r.v[2].x; acc[j][2][1] += r.v[2].y;
-        acc[j][2][2] += r.v[2].z; acc[j][2][3] += r.v[2].w;
-        lgkm_wait1<0>(r.v[3]);
-        acc[j][3][0] += r.v[3].x; acc[j][3][1] += r.v[3].y;
-        acc[j][3][2] += r.v[3].z; acc[j][3][3] += r.v[3].w;
+          for (int g2 = 0; g2 < G; ++g2)
+            v[j][g2] = *(const lds_f32x4_t*)(uintptr_t)(cb + (uint32_t)(ov[j] * 16) + g2 * 1024);
+#pragma unroll
+        for (int j = 0; j < DPW; ++j)
+#pragma unroll
+          for (int g2 = 0; g2 < G; ++g2) {
+            acc[j][g2][0] += v[j][g2].x;
+            acc[j][g2][1] += v[j][g2].y;
+            acc[j][g2][2] += v[j][g2].z;
+            acc[j][g2][3] += v[j][g2].w;
+          }
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * G, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 4 * G, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, G, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 4 * G, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, G, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 4 * G, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 4 * G, 0);
       }
     }
+  }
+  if (stamps) ts_comp += __builtin_amdgcn_s_memtime() - tB;
+  if (stamps) {
+    if (lane == 0) {
+      float* o = out + ((int64_t)blockIdx.x * (NCW + NLW) + w) * 4;
+      o[0] = 0.f; o[1] = (float)ts_poll; o[2] = (float)ts_comp; o[3] = 1.f;
+    }
+    return;
   }
   const int d0 = dblk * DB + w * DPW;
 #pragma unroll
@@ -1463,7 +1537,11 @@ struct Variant {
 
 // Candidate tilings, best first; the plan takes the first whose LDS ring fits
 // the budget.
-static const Variant kF32Variants[] = {{false, 4, 4, 4, 8, 2, 3, false, 0, 2, 1},
+static const Variant kF32Variants[] = {{false, 4, 4, 4, 14, 2, 4, false, 0, 2, 1},
+                                       {false, 4, 4, 4, 14, 1, 8, false, 0, 2, 1},
+                                       {false, 4, 4, 4, 8, 1, 6, false, 0, 2, 1},
+                                       {false, 4, 4, 4, 12, 1, 8, false, 0, 4, 1},
+                                       {false, 4, 4, 4, 8, 2, 3, false, 0, 2, 1},
                                        {false, 4, 4, 4, 8, 2, 3, false, 0, 1},
                                        {false, 4, 4, 4, 8, 2, 3, false, 0, 2},
                                        {false, 4, 4, 4, 8, 2, 2, false, 0},
@@ -1472,15 +1550,33 @@ static const Variant kF32Variants[] = {{false, 4, 4, 4, 8, 2, 3, false, 0, 2, 1}
                                        {false, 4, 4, 4, 8, 2, 3, true, 0},
                                        {false, 4, 4, 1, 8, 1, 2, false, 0},
                                        {false, 4, 1, 1, 1, 1, 2, false, 0}};
-static const Variant kU8Variants[] = {{false, 4, 4, 4, 8, 2, 3, false, 0, 2, 1},
+static const Variant kU8Variants[] = {{false, 4, 4, 4, 14, 2, 4, false, 0, 2, 1},
                                       {true, 8, 2, 4, 8, 4, 2, false},
                                       {true, 8, 2, 4, 8, 2, 2, false},
                                       {true, 8, 2, 1, 8, 1, 2, false},
                                       {true, 8, 1, 1, 1, 1, 2, false}};
 
 // LDS per workgroup: 16-wave tiles run one per CU, 8-wave tiles two per CU
-static int64_t lds_budget(const Variant& v) { return v.NW >= 16 ? 150 * 1024 : 76 * 1024; }
+static int64_t lds_budget(const Variant& v) {
+  if (v.il) return (v.NW + v.ws) * 2 <= 16 ? 78 * 1024 : 158 * 1024;  // 2 or 1 workgroups per CU
+  return v.NW >= 16 ? 150 * 1024 : 76 * 1024;
+}
 static constexpr int kLdsMax = 160 * 1024;
+
+typedef void (*sweep_il_fn)(const float4*, int64_t, int, int, const int*, float*, int64_t, int,
+                            int64_t, int64_t, int64_t, int, int, int, int);
+static sweep_il_fn il_kernel_for(const Variant& v) {
+#define IL(NCW_, NLW_, CC_, NB_)                                                             \
+  if (v.NW == NCW_ && v.ws == NLW_ && v.CC == CC_ && v.NBUF == NB_ && v.G == 4 && v.DPW == 4) \
+    return k_sweep_il<4, 4, NCW_, NLW_, CC_, NB_>;
+  IL(14, 2, 1, 8)
+  IL(14, 2, 2, 4)
+  IL(8, 2, 1, 6)
+  IL(12, 4, 1, 8)
+  IL(8, 2, 2, 3)
+#undef IL
+  return nullptr;
+}
 
 typedef void (*sweep_fn)(const void*, int64_t, int, int64_t, const int*, int, int, const int*,
                          const int*, int, const float*, float*, int64_t, int64_t, int, int, int,
@@ -1584,8 +1680,8 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
     const int64_t n_tblk = Qs / Tq;
     const int64_t blocks = n_tblk * p->n_dblk;
     if (blocks >= (1ll << 31)) { rc = -1; break; }
-    hipLaunchKernelGGL((k_sweep_il<4, 4, 8, 2, 2, 3>), dim3((unsigned)blocks), dim3(p->v.threads()),
-                       p->lds_bytes, st, R, nR, (int)C, (int)lo, p->d_tab, p->d_bmin, out, ld_out,
+    hipLaunchKernelGGL(il_kernel_for(p->v), dim3((unsigned)blocks), dim3(p->v.threads()),
+                       p->lds_bytes, st, R, nR, (int)C, (int)lo, p->d_tab, out, ld_out,
                        (int)p->D, Qs, t_base, t_base + cnt, p->stride, (int)n_tblk,
                        (int)p->n_dblk, dbg);
     if (hipGetLastError() != hipSuccess) rc = -3;
@@ -1605,7 +1701,7 @@ int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int d
               "pdd_sweep_plan_create: bad extents D=%lld C=%lld", (long long)D, (long long)C);
   PDD_REQUIRE(dtype == PDD_F32 || dtype == PDD_U8, "pdd_sweep_plan_create: dtype must be F32 or U8");
   const Variant* cands = dtype == PDD_U8 ? kU8Variants : kF32Variants;
-  const int ncand = dtype == PDD_U8 ? 5 : 9;
+  const int ncand = dtype == PDD_U8 ? 5 : 13;
 
   const int fv = forced_variant();
   for (int vi = (fv >= 0 && fv < ncand) ? fv : 0; vi < ncand; ++vi) {
@@ -1670,7 +1766,9 @@ int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int d
     // linear kernel: metadata rings (NBUF x 64 ints x 2) after the buffers
     const int64_t need = v.ring ? lds_budget(v)
                                 : per_chan * v.CC + (v.lin ? 2 * v.NBUF * 64 * 4 : 0) +
-                                      (v.ws ? v.NBUF * 64 * 4 : 0);
+                                      (v.il   ? il_meta_bytes(v.ws, v.NBUF, v.CC, v.DB())
+                                       : v.ws ? v.NBUF * 64 * 4
+                                              : 0);
     if (v.il && (int64_t)max_span + 64 * v.G > (int64_t)1 << 20) continue;  // windows too wide
     if (need > lds_budget(v) && !(last && need <= kLdsMax)) {
       if (last) {
@@ -1692,7 +1790,19 @@ int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int d
     p->lds_bytes = (int)need;
     p->P = ringP;
     p->dtype = dtype;
-    if (v.lin || v.ws) {
+    if (v.il) {
+      // mt[dblk][c][DB + 4] = shifts rel. to bmin, then {bmin, span, 0, 0}
+      const int64_t ROWN = DB + 4;
+      std::vector<int> mtv((size_t)(n_dblk * C * ROWN), 0);
+      for (int64_t b = 0; b < n_dblk; ++b)
+        for (int64_t c = 0; c < C; ++c) {
+          const size_t base = (size_t)((b * C + c) * ROWN);
+          for (int64_t d = 0; d < DB; ++d) mtv[base + d] = tab[(size_t)(c * Dpad + b * DB + d)];
+          mtv[base + DB] = bmin[(size_t)(b * C + c)];
+          mtv[base + DB + 1] = bspan[(size_t)(b * C + c)];
+        }
+      tab.swap(mtv);
+    } else if (v.lin || v.ws) {
       // block-major layouts read by per-chunk metadata DMAs:
       //   rel [dblk][c][DB], meta[dblk][c] = {bmin, span}
       std::vector<int> relb((size_t)(n_dblk * C * DB));
@@ -1723,7 +1833,7 @@ int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int d
     }
     if (p->lds_bytes > 64 * 1024) {
       const void* kf = v.ring ? (const void*)k_sweep_ring<4, 4, 8>
-                              : v.il ? (const void*)k_sweep_il<4, 4, 8, 2, 2, 3>
+                              : v.il ? (const void*)il_kernel_for(v)
                                      : (const void*)kernel_for(v);
       e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, p->lds_bytes);
       if (e != hipSuccess) {
