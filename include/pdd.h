@@ -34,8 +34,10 @@ enum {
   PDD_PAD_VALUE = 0,  /* per-channel pad value from `padvals` (number / 'mean' / 'median') */
   PDD_PAD_ROTATE = 1  /* psr_utils.rotate wrap-around (padval == 'rotate') */
 };
-/* channel statistics (pad values for 'mean'/'median', spectra.py:83-86) */
-enum { PDD_STAT_MEAN = 0, PDD_STAT_MEDIAN = 1 };
+/* channel statistics: pad values for 'mean'/'median' (spectra.py:83-86);
+ * std (population, float64 two-pass), min, max for scaled/scaled2
+ * (spectra.py:140-188) */
+enum { PDD_STAT_MEAN = 0, PDD_STAT_MEDIAN = 1, PDD_STAT_STD = 2, PDD_STAT_MIN = 3, PDD_STAT_MAX = 4 };
 /* zero-DM layouts */
 enum { PDD_LAYOUT_TIME_MAJOR = 0, /* [nspec][nchan], filterbank file order */
        PDD_LAYOUT_CHAN_MAJOR = 1  /* [nchan][nspec], Spectra.data order    */ };
@@ -58,8 +60,10 @@ int pdd_corner_turn(const void* in, int in_dtype, int64_t nspec, int64_t nchan, 
 int pdd_convert_f32(const void* in, int in_dtype, int64_t rows, int64_t cols, int64_t ld_in,
                     float* out, int64_t ld_out, void* stream);
 
-/* Per-channel mean or median of x[C][N] -> out[C] (float32).
- * Pad values of Spectra.shift_channels 'mean'/'median' (formats/spectra.py:83-86). */
+/* Per-channel statistic of x[C][N] -> out[C] (float32): mean / median (pad
+ * values of Spectra.shift_channels 'mean'/'median', formats/spectra.py:83-86;
+ * Spectra.masked maskvals, spectra.py:216-222), std / min / max
+ * (Spectra.scaled / scaled2 per-channel terms, spectra.py:157-187). */
 int pdd_channel_stats(const float* x, int64_t C, int64_t N, int64_t ld, int stat,
                       float* out, void* stream);
 
@@ -91,6 +95,28 @@ int pdd_downsample(const float* x, int64_t C, int64_t N, int64_t ld, int64_t fac
  * `out` may alias `in`. */
 int pdd_zero_dm(const void* in, int dtype, int64_t nspec, int64_t nchan, int64_t ld,
                 int layout, void* out, int64_t ld_out, void* stream);
+
+/* ---- waterfaller post-chain (Spectra.scaled / scaled2 / masked / smooth) ---- */
+/* Whole-array statistics of x[C][N] into out4 (device float[4]):
+ * {mean, population std, min, max}, float64 accumulation.
+ * Replaces other.data.std() / other.data.max() (formats/spectra.py:156, 181). */
+int pdd_global_stats(const float* x, int64_t C, int64_t N, int64_t ld, float* out4, void* stream);
+/* out[c][t] = (x[c][t] - sub[c*sub_inc]) / div[c*div_inc] (inc 0 = broadcast).
+ * Replaces the per-channel loops of Spectra.scaled (formats/spectra.py:157-162)
+ * and Spectra.scaled2 (spectra.py:182-187). */
+int pdd_scale_rows(const float* x, int64_t C, int64_t N, int64_t ld, const float* sub,
+                   int64_t sub_inc, const float* div, int64_t div_inc, float* out, int64_t ld_out,
+                   void* stream);
+/* out[c][t] = mask[c][t] ? vals[c] : x[c][t]  (mask: uint8 0/1).
+ * Replaces np.where(mask, maskvals, data) of Spectra.masked (formats/spectra.py:225-226). */
+int pdd_masked_fill(const float* x, int64_t C, int64_t N, int64_t ld, const uint8_t* mask,
+                    int64_t ld_mask, const float* vals, float* out, int64_t ld_out, void* stream);
+/* Boxcar of `width` samples and height 1/sqrt(width), 'same' centring, per
+ * channel, padded with padvals[c] (PDD_PAD_VALUE: number / 'mean' / 'median')
+ * or wrapped (PDD_PAD_ROTATE: 'wrap').  Replaces Spectra.smooth
+ * (formats/spectra.py:262-303; scipy.signal.convolve). `out` must not alias x. */
+int pdd_smooth(const float* x, int64_t C, int64_t N, int64_t ld, int64_t width, int pad_mode,
+               const float* padvals, float* out, int64_t ld_out, void* stream);
 
 /* ---- batched DM sweep (new executor over utils/DDplan2b.py grids) ----
  * plane[d][t] = sum_c X(c, t + table[d][c]), t < n_out (defaults of

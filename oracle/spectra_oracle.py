@@ -212,3 +212,94 @@ def sweep_plane(data, table, padval=0, n_out=None):
     if n_out is None:
         n_out = N - max(0, int(np.max(table)))
     return np.array([shifted_sum(data, table[d], padval)[:n_out] for d in range(table.shape[0])])
+
+
+# --------------------------------------------------------------------------
+# waterfaller post-chain (formats/spectra.py:140-227, 262-303)
+# --------------------------------------------------------------------------
+
+
+def scaled(data, indep=False):
+    """Spectra.scaled, spectra.py:140-163: per channel (chan - median) / std,
+    std of the whole array (indep=False) or of the channel (indep=True)."""
+    out = np.array(data, dtype=np.float64, copy=True)
+    if not indep:
+        std = out.std()
+    for ii in range(out.shape[0]):
+        chan = out[ii]
+        median = np.median(chan)
+        if indep:
+            std = chan.std()
+        chan[:] = (chan - median) / std
+    return out
+
+
+def scaled2(data, indep=False):
+    """Spectra.scaled2, spectra.py:165-188: (chan - chan.min()) / max, max of
+    the whole array (indep=False) or of the channel."""
+    out = np.array(data, dtype=np.float64, copy=True)
+    if not indep:
+        mx = out.max()
+    for ii in range(out.shape[0]):
+        chan = out[ii]
+        mn = chan.min()
+        if indep:
+            mx = chan.max()
+        chan[:] = (chan - mn) / mx
+    return out
+
+
+def mask_values(data, maskval="median-mid80"):
+    """Per-channel replacement values of Spectra.masked, spectra.py:211-224.
+    'median-mid80' is the median of sorted(chan)[n:-n], n = round(0.1 N):
+    symmetric trimming keeps the median, except n == 0, where the slice is
+    empty and the reference gets NaN."""
+    data = np.asarray(data, dtype=np.float64)
+    C, N = data.shape
+    vals = np.ones(C)
+    for ii in range(C):
+        chan = data[ii]
+        if maskval == "mean":
+            vals[ii] = np.mean(chan)
+        elif maskval == "median":
+            vals[ii] = np.median(chan)
+        elif maskval == "median-mid80":
+            n = int(np.round(0.1 * N))
+            vals[ii] = np.median(np.sort(chan)[n:-n]) if n > 0 else np.nan
+        else:
+            vals[ii] = maskval
+    return vals
+
+
+def masked(data, mask, maskval="median-mid80"):
+    """Spectra.masked, spectra.py:190-227."""
+    data = np.asarray(data, dtype=np.float64)
+    assert data.shape == mask.shape
+    vals = mask_values(data, maskval)
+    return np.where(mask, np.ones_like(data) * vals[:, np.newaxis], data)
+
+
+def smooth(data, width=1, padval=0):
+    """Spectra.smooth, spectra.py:262-303: per channel, pad `width` samples on
+    each side ('wrap', 'mean', 'median' or a number), convolve with a boxcar of
+    height 1/sqrt(width) ('same' centring), keep the middle N samples."""
+    out = np.array(data, dtype=np.float64, copy=True)
+    if width <= 1:
+        return out
+    kernel = np.ones(width) / np.sqrt(width)
+    N = out.shape[1]
+    for ii in range(out.shape[0]):
+        chan = out[ii]
+        if padval == "wrap":
+            tosmooth = np.concatenate([chan[-width:], chan, chan[:width]])
+        else:
+            if padval == "mean":
+                pv = np.mean(chan)
+            elif padval == "median":
+                pv = np.median(chan)
+            else:
+                pv = padval
+            tosmooth = np.ones(N + 2 * width) * pv
+            tosmooth[width:-width] = chan
+        chan[:] = np.convolve(tosmooth, kernel, "same")[width:-width]
+    return out

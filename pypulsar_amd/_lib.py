@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(_HERE, "libpdd.so")
 # element types / modes (include/pdd.h)
 F32, U8, U16 = 0, 1, 2
 PAD_VALUE, PAD_ROTATE = 0, 1
-STAT_MEAN, STAT_MEDIAN = 0, 1
+STAT_MEAN, STAT_MEDIAN, STAT_STD, STAT_MIN, STAT_MAX = 0, 1, 2, 3, 4
 LAYOUT_TIME_MAJOR, LAYOUT_CHAN_MAJOR = 0, 1
 
 # every symbol include/pdd.h declares (checked by tests/test_abi.py)
@@ -25,7 +25,8 @@ EXPORTS = (
     "pdd_version", "pdd_last_error", "pdd_sync", "pdd_corner_turn", "pdd_convert_f32",
     "pdd_channel_stats", "pdd_shift_pad", "pdd_shift_group_sum", "pdd_downsample",
     "pdd_zero_dm", "pdd_sweep_plan_create", "pdd_sweep_execute", "pdd_sweep_plan_info",
-    "pdd_sweep_plan_destroy",
+    "pdd_sweep_plan_destroy", "pdd_global_stats", "pdd_scale_rows", "pdd_masked_fill",
+    "pdd_smooth",
 )
 
 
@@ -56,6 +57,10 @@ _SIGS = {
     "pdd_sweep_execute": ([_vp, _vp, _i64, _i64, _int, _vp, _vp, _i64, _i64, _vp], _int),
     "pdd_sweep_plan_info": ([_vp, _vp], _int),
     "pdd_sweep_plan_destroy": ([_vp], _int),
+    "pdd_global_stats": ([_vp, _i64, _i64, _i64, _vp, _vp], _int),
+    "pdd_scale_rows": ([_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp], _int),
+    "pdd_masked_fill": ([_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _i64, _vp], _int),
+    "pdd_smooth": ([_vp, _i64, _i64, _i64, _i64, _int, _vp, _vp, _i64, _vp], _int),
 }
 
 

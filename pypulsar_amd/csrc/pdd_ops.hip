@@ -281,6 +281,210 @@ __global__ __launch_bounds__(256) void k_zero_dm_cm(const T* __restrict__ in, in
   for (int64_t c = 0; c < nchan; ++c) out[c * ld_out + t] = zd_apply<T>(in[c * ld + t], mean);
 }
 
+// ---------------------------------------------------------------- waterfaller post-chain
+// (Spectra.scaled / scaled2 / masked / smooth, formats/spectra.py:140-303)
+
+// Per-channel population std (two passes in float64) or min / max.
+__global__ __launch_bounds__(256) void k_channel_std(const float* __restrict__ x, int64_t N,
+                                                     int64_t ld, float* __restrict__ out) {
+  __shared__ double part[4];
+  __shared__ double mean_s;
+  const float* row = x + (int64_t)blockIdx.x * ld;
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < N; i += 256) s += (double)row[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) mean_s = ((part[0] + part[1]) + (part[2] + part[3])) / (double)N;
+  __syncthreads();
+  const double m = mean_s;
+  double q = 0.0;
+  for (int64_t i = threadIdx.x; i < N; i += 256) {
+    const double d = (double)row[i] - m;
+    q += d * d;
+  }
+  q = wave_sum(q);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = q;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = (float)sqrt(((part[0] + part[1]) + (part[2] + part[3])) / (double)N);
+}
+
+__device__ __forceinline__ float wave_minmax(float v, bool want_max) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float u = __shfl_down(v, o, 64);
+    v = want_max ? fmaxf(v, u) : fminf(v, u);
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(256) void k_channel_minmax(const float* __restrict__ x, int64_t N,
+                                                        int64_t ld, int want_max,
+                                                        float* __restrict__ out) {
+  __shared__ float part[4];
+  const float* row = x + (int64_t)blockIdx.x * ld;
+  float v = want_max ? -INFINITY : INFINITY;
+  for (int64_t i = threadIdx.x; i < N; i += 256) v = want_max ? fmaxf(v, row[i]) : fminf(v, row[i]);
+  v = wave_minmax(v, want_max);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = part[0];
+    for (int i = 1; i < 4; ++i) r = want_max ? fmaxf(r, part[i]) : fminf(r, part[i]);
+    out[blockIdx.x] = r;
+  }
+}
+
+// Global statistics of a [C][N] array: fixed grid (kGlobBlocks x 256), every
+// partial in float64, combined in a fixed order (deterministic).
+constexpr int kGlobBlocks = 1024;
+
+__global__ __launch_bounds__(256) void k_global_partial(const float* __restrict__ x, int64_t C,
+                                                        int64_t N, int64_t ld, int pass,
+                                                        const double* __restrict__ fin,
+                                                        double* __restrict__ part) {
+  __shared__ double ps[4][3];
+  const int64_t total = C * N;
+  const double m = pass ? fin[0] : 0.0;
+  double a = 0.0, mn = INFINITY, mx = -INFINITY;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)kGlobBlocks * 256) {
+    const double v = (double)x[(i / N) * ld + (i % N)];
+    if (pass) {
+      a += (v - m) * (v - m);
+    } else {
+      a += v;
+      mn = fmin(mn, v);
+      mx = fmax(mx, v);
+    }
+  }
+  a = wave_sum(a);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = fmin(mn, __shfl_down(mn, o, 64));
+    mx = fmax(mx, __shfl_down(mx, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    ps[threadIdx.x >> 6][0] = a;
+    ps[threadIdx.x >> 6][1] = mn;
+    ps[threadIdx.x >> 6][2] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[blockIdx.x * 3 + 0] = (ps[0][0] + ps[1][0]) + (ps[2][0] + ps[3][0]);
+    part[blockIdx.x * 3 + 1] = fmin(fmin(ps[0][1], ps[1][1]), fmin(ps[2][1], ps[3][1]));
+    part[blockIdx.x * 3 + 2] = fmax(fmax(ps[0][2], ps[1][2]), fmax(ps[2][2], ps[3][2]));
+  }
+}
+
+// pass 0: fin[0] = mean, out[0] = mean, out[2] = min, out[3] = max;
+// pass 1: out[1] = population std
+__global__ __launch_bounds__(256) void k_global_reduce(const double* __restrict__ part, int pass,
+                                                       int64_t total, double* __restrict__ fin,
+                                                       float* __restrict__ out) {
+  __shared__ double ps[4][3];
+  double a = 0.0, mn = INFINITY, mx = -INFINITY;
+  for (int i = threadIdx.x; i < kGlobBlocks; i += 256) {
+    a += part[i * 3 + 0];
+    mn = fmin(mn, part[i * 3 + 1]);
+    mx = fmax(mx, part[i * 3 + 2]);
+  }
+  a = wave_sum(a);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = fmin(mn, __shfl_down(mn, o, 64));
+    mx = fmax(mx, __shfl_down(mx, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    ps[threadIdx.x >> 6][0] = a;
+    ps[threadIdx.x >> 6][1] = mn;
+    ps[threadIdx.x >> 6][2] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double s = (ps[0][0] + ps[1][0]) + (ps[2][0] + ps[3][0]);
+    if (pass == 0) {
+      fin[0] = s / (double)total;
+      out[0] = (float)(s / (double)total);
+      out[2] = (float)fmin(fmin(ps[0][1], ps[1][1]), fmin(ps[2][1], ps[3][1]));
+      out[3] = (float)fmax(fmax(ps[0][2], ps[1][2]), fmax(ps[2][2], ps[3][2]));
+    } else {
+      out[1] = (float)sqrt(s / (double)total);
+    }
+  }
+}
+
+// out[c][t] = (x[c][t] - sub[c * sub_inc]) / div[c * div_inc]  (float64 arithmetic)
+__global__ __launch_bounds__(256) void k_scale_rows(const float* __restrict__ x, int64_t N,
+                                                    int64_t ld, const float* __restrict__ sub,
+                                                    int64_t sub_inc, const float* __restrict__ dv,
+                                                    int64_t div_inc, float* __restrict__ out,
+                                                    int64_t ld_out, int64_t tiles) {
+  const int64_t c = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const double s = (double)sub[c * sub_inc], d = (double)dv[c * div_inc];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t t = tile * 1024 + k * 256 + threadIdx.x;
+    if (t < N) out[c * ld_out + t] = (float)(((double)x[c * ld + t] - s) / d);
+  }
+}
+
+// out = mask ? vals[c] : x
+__global__ __launch_bounds__(256) void k_masked_fill(const float* __restrict__ x, int64_t N,
+                                                     int64_t ld, const uint8_t* __restrict__ mask,
+                                                     int64_t ld_mask, const float* __restrict__ vals,
+                                                     float* __restrict__ out, int64_t ld_out,
+                                                     int64_t tiles) {
+  const int64_t c = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const float v = vals[c];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t t = tile * 1024 + k * 256 + threadIdx.x;
+    if (t < N) out[c * ld_out + t] = mask[c * ld_mask + t] ? v : x[c * ld + t];
+  }
+}
+
+// Boxcar smooth: out[c][t] = (1/sqrt(w)) * sum_{j = t - w/2}^{t + (w-1)/2} P(c, j)
+// with P the padded channel (value pad, or wrap for PDD_PAD_ROTATE).  The
+// window of one 1024-output tile is staged in LDS (w <= kSmoothLds - 1023);
+// sums in float64.
+constexpr int kSmoothLds = 8192;
+
+__device__ __forceinline__ float smooth_src(const float* row, int64_t j, int64_t N, int pad_mode,
+                                            float pad) {
+  if (j >= 0 && j < N) return row[j];
+  if (pad_mode == PDD_PAD_ROTATE) {
+    int64_t r = j % N;
+    return row[r < 0 ? r + N : r];
+  }
+  return pad;
+}
+
+__global__ __launch_bounds__(256) void k_smooth(const float* __restrict__ x, int64_t N, int64_t ld,
+                                                int64_t w, int pad_mode,
+                                                const float* __restrict__ padvals,
+                                                float* __restrict__ out, int64_t ld_out,
+                                                int64_t tiles) {
+  __shared__ float win[kSmoothLds];
+  const int64_t c = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const float* row = x + c * ld;
+  const float pad = (pad_mode == PDD_PAD_VALUE) ? padvals[c] : 0.f;
+  const int64_t t0 = tile * 1024;
+  const int64_t j0 = t0 - w / 2;
+  const int64_t nw = 1024 + w - 1;
+  for (int64_t i = threadIdx.x; i < nw; i += 256) win[i] = smooth_src(row, j0 + i, N, pad_mode, pad);
+  __syncthreads();
+  const double k = 1.0 / sqrt((double)w);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t o = q * 256 + threadIdx.x;
+    if (t0 + o >= N) continue;
+    double s = 0.0;
+    for (int64_t i = 0; i < w; ++i) s += (double)win[o + i];
+    out[c * ld_out + t0 + o] = (float)(s * k);
+  }
+}
+
 static int grid_1d(int64_t n, int per_block = 256) {
   int64_t g = cdiv(n, per_block);
   if (g > 2048 * 8) g = 2048 * 8;
@@ -364,6 +568,10 @@ int pdd_channel_stats(const float* x, int64_t C, int64_t N, int64_t ld, int stat
     k_channel_mean<<<(unsigned)C, 256, 0, s>>>(x, N, ld, out);
   else if (stat == PDD_STAT_MEDIAN)
     k_channel_median<<<(unsigned)C, 256, 0, s>>>(x, N, ld, out);
+  else if (stat == PDD_STAT_STD)
+    k_channel_std<<<(unsigned)C, 256, 0, s>>>(x, N, ld, out);
+  else if (stat == PDD_STAT_MIN || stat == PDD_STAT_MAX)
+    k_channel_minmax<<<(unsigned)C, 256, 0, s>>>(x, N, ld, stat == PDD_STAT_MAX, out);
   else
     PDD_REQUIRE(false, "pdd_channel_stats: bad stat %d", stat);
   PDD_LAUNCHED();
@@ -450,6 +658,71 @@ int pdd_zero_dm(const void* in, int dtype, int64_t nspec, int64_t nchan, int64_t
   } else {
     PDD_REQUIRE(false, "pdd_zero_dm: bad layout %d", layout);
   }
+  PDD_LAUNCHED();
+  return 0;
+}
+
+int pdd_global_stats(const float* x, int64_t C, int64_t N, int64_t ld, float* out4, void* stream) {
+  PDD_REQUIRE(x && out4, "pdd_global_stats: null pointer");
+  PDD_REQUIRE(C > 0 && N > 0 && ld >= N, "pdd_global_stats: bad shape");
+  hipStream_t s = as_stream(stream);
+  double* scratch = nullptr;
+  PDD_HIP(hipMallocAsync((void**)&scratch, (kGlobBlocks * 3 + 1) * sizeof(double), s));
+  double* fin = scratch + kGlobBlocks * 3;
+  k_global_partial<<<kGlobBlocks, 256, 0, s>>>(x, C, N, ld, 0, fin, scratch);
+  k_global_reduce<<<1, 256, 0, s>>>(scratch, 0, C * N, fin, out4);
+  k_global_partial<<<kGlobBlocks, 256, 0, s>>>(x, C, N, ld, 1, fin, scratch);
+  k_global_reduce<<<1, 256, 0, s>>>(scratch, 1, C * N, fin, out4);
+  const hipError_t e = hipGetLastError();
+  (void)hipFreeAsync(scratch, s);
+  PDD_REQUIRE(e == hipSuccess, "pdd_global_stats: launch failed: %s", hipGetErrorString(e));
+  return 0;
+}
+
+int pdd_scale_rows(const float* x, int64_t C, int64_t N, int64_t ld, const float* sub,
+                   int64_t sub_inc, const float* div, int64_t div_inc, float* out, int64_t ld_out,
+                   void* stream) {
+  PDD_REQUIRE(x && out && sub && div, "pdd_scale_rows: null pointer");
+  PDD_REQUIRE(C >= 0 && N >= 0 && ld >= N && ld_out >= N && sub_inc >= 0 && div_inc >= 0,
+              "pdd_scale_rows: bad shape");
+  if (C == 0 || N == 0) return 0;
+  const int64_t tiles = cdiv(N, 1024);
+  PDD_REQUIRE(C * tiles < (1ll << 31), "pdd_scale_rows: too large");
+  k_scale_rows<<<(unsigned)(C * tiles), 256, 0, as_stream(stream)>>>(x, N, ld, sub, sub_inc, div,
+                                                                     div_inc, out, ld_out, tiles);
+  PDD_LAUNCHED();
+  return 0;
+}
+
+int pdd_masked_fill(const float* x, int64_t C, int64_t N, int64_t ld, const uint8_t* mask,
+                    int64_t ld_mask, const float* vals, float* out, int64_t ld_out, void* stream) {
+  PDD_REQUIRE(x && out && mask && vals, "pdd_masked_fill: null pointer");
+  PDD_REQUIRE(C >= 0 && N >= 0 && ld >= N && ld_mask >= N && ld_out >= N,
+              "pdd_masked_fill: bad shape");
+  if (C == 0 || N == 0) return 0;
+  const int64_t tiles = cdiv(N, 1024);
+  PDD_REQUIRE(C * tiles < (1ll << 31), "pdd_masked_fill: too large");
+  k_masked_fill<<<(unsigned)(C * tiles), 256, 0, as_stream(stream)>>>(x, N, ld, mask, ld_mask, vals,
+                                                                      out, ld_out, tiles);
+  PDD_LAUNCHED();
+  return 0;
+}
+
+int pdd_smooth(const float* x, int64_t C, int64_t N, int64_t ld, int64_t width, int pad_mode,
+               const float* padvals, float* out, int64_t ld_out, void* stream) {
+  PDD_REQUIRE(x && out, "pdd_smooth: null pointer");
+  PDD_REQUIRE(x != out, "pdd_smooth: out must not alias x");
+  PDD_REQUIRE(C >= 0 && N > 0 && ld >= N && ld_out >= N, "pdd_smooth: bad shape");
+  PDD_REQUIRE(width >= 1 && width <= kSmoothLds - 1023, "pdd_smooth: width %lld out of range",
+              (long long)width);
+  PDD_REQUIRE(pad_mode == PDD_PAD_ROTATE || (pad_mode == PDD_PAD_VALUE && padvals),
+              "pdd_smooth: bad pad mode %d", pad_mode);
+  PDD_REQUIRE(pad_mode != PDD_PAD_ROTATE || width <= N, "pdd_smooth: wrap needs width <= N");
+  if (C == 0) return 0;
+  const int64_t tiles = cdiv(N, 1024);
+  PDD_REQUIRE(C * tiles < (1ll << 31), "pdd_smooth: too large");
+  k_smooth<<<(unsigned)(C * tiles), 256, 0, as_stream(stream)>>>(x, N, ld, width, pad_mode, padvals,
+                                                                 out, ld_out, tiles);
   PDD_LAUNCHED();
   return 0;
 }

@@ -259,6 +259,110 @@ class Spectra(object):
         self.numspectra = new_num_spectra
         self.dt = self.dt * factor
 
+    # ------------------------------------------------------------ post-chain
+    # waterfaller.py:120-127 continues with scaled() and smooth(); masked() is
+    # its rfifind mask step (waterfaller.py:92-99).  All return / modify the
+    # device data like the reference (copies vs in place as documented there).
+    def _stat(self, x, stat):
+        v = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
+        call("pdd_channel_stats", ptr(x), x.shape[0], x.shape[1], x.stride(0), stat, ptr(v),
+             stream_ptr())
+        return v
+
+    def _global(self, x):
+        g = torch.empty(4, dtype=torch.float32, device=x.device)  # mean, std, min, max
+        call("pdd_global_stats", ptr(x), x.shape[0], x.shape[1], x.stride(0), ptr(g), stream_ptr())
+        return g
+
+    def _scale(self, x, sub, sub_inc, div, div_inc):
+        C, N = x.shape
+        out = torch.empty((C, N), dtype=torch.float32, device=x.device)
+        call("pdd_scale_rows", ptr(x), C, N, x.stride(0), ptr(sub), sub_inc, ptr(div), div_inc,
+             ptr(out), N, stream_ptr())
+        return out
+
+    def scaled(self, indep=False):
+        """Copy with every channel minus its median, divided by the global
+        std (indep=False) or the channel's std (spectra.py:140-163)."""
+        other = copy.deepcopy(self)
+        x = other._x
+        if x.numel() == 0:
+            return other
+        med = self._stat(x, _lib.STAT_MEDIAN)
+        if indep:
+            std, inc = self._stat(x, _lib.STAT_STD), 1
+        else:
+            std, inc = self._global(x)[1:2], 0
+        other._set(self._scale(x, med, 1, std, inc))
+        return other
+
+    def scaled2(self, indep=False):
+        """Copy with every channel minus its minimum, divided by the global
+        maximum (indep=False) or the channel's maximum (spectra.py:165-188)."""
+        other = copy.deepcopy(self)
+        x = other._x
+        if x.numel() == 0:
+            return other
+        mn = self._stat(x, _lib.STAT_MIN)
+        if indep:
+            mx, inc = self._stat(x, _lib.STAT_MAX), 1
+        else:
+            mx, inc = self._global(x)[3:4], 0
+        other._set(self._scale(x, mn, 1, mx, inc))
+        return other
+
+    def masked(self, mask, maskval="median-mid80"):
+        """Copy with masked entries replaced by ``maskval`` per channel: a
+        number, 'mean', 'median' or 'median-mid80' (spectra.py:190-227).
+        'median-mid80' is the median of the middle 80% of the sorted channel,
+        which equals the channel median, except when round(0.1 N) == 0, where
+        the reference's slice is empty and its value is NaN."""
+        mask = np.asarray(mask)
+        assert (self.numchans, self.numspectra) == mask.shape
+        other = copy.deepcopy(self)
+        x = other._x
+        C, N = x.shape
+        if C == 0 or N == 0:
+            return other
+        if maskval == "mean":
+            vals = self._stat(x, _lib.STAT_MEAN)
+        elif maskval in ("median", "median-mid80"):
+            if maskval == "median-mid80" and int(np.round(0.1 * self.numspectra)) == 0:
+                vals = torch.full((C,), float("nan"), dtype=torch.float32, device=x.device)
+            else:
+                vals = self._stat(x, _lib.STAT_MEDIAN)
+        else:
+            vals = torch.full((C,), float(maskval), dtype=torch.float32, device=x.device)
+        m = torch.from_numpy(np.ascontiguousarray(mask, dtype=np.uint8)).to(x.device)
+        out = torch.empty((C, N), dtype=torch.float32, device=x.device)
+        call("pdd_masked_fill", ptr(x), C, N, x.stride(0), ptr(m), N, ptr(vals), ptr(out), N,
+             stream_ptr())
+        other._set(out)
+        return other
+
+    def smooth(self, width=1, padval=0):
+        """In place: convolve every channel with a boxcar of ``width`` samples
+        and height 1/sqrt(width); overlap values from ``padval`` (a number,
+        'mean', 'median' or 'wrap') (spectra.py:262-303)."""
+        if width <= 1:
+            return
+        x = self._x
+        C, N = x.shape
+        if C == 0 or N == 0:
+            return
+        if padval == "wrap":
+            mode, pv = _lib.PAD_ROTATE, None
+        elif padval in ("mean", "median"):
+            mode, pv = _lib.PAD_VALUE, self._stat(x, _lib.STAT_MEAN if padval == "mean"
+                                                   else _lib.STAT_MEDIAN)
+        else:
+            mode = _lib.PAD_VALUE
+            pv = torch.full((C,), float(padval), dtype=torch.float32, device=x.device)
+        out = torch.empty((C, N), dtype=torch.float32, device=x.device)
+        call("pdd_smooth", ptr(x), C, N, x.stride(0), int(width), mode, ptr(pv), ptr(out), N,
+             stream_ptr())
+        self._set(out)
+
     # ------------------------------------------------------------ fused extras
     def sum_channels(self):
         """Device float32 [numspectra] series = data.sum(axis=0)
