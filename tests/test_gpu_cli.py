@@ -1,0 +1,98 @@
+"""The drop-in CLIs on the GPU: zero_dm_filter, mockspecfil2subbands and
+waterfaller (bin/*.py of the reference) end to end on synthetic filterbanks,
+checked against the oracle restatement of the reference's per-spectrum /
+per-channel loops."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import band, rel_err, u8_data
+from oracle import spectra_oracle as orc
+
+pytestmark = pytest.mark.gpu
+DT = 64e-6
+
+
+def _fil(tmp_path, x_tc, nbits=8, C=None, foff=None, name="in.fil"):
+    from pypulsar_amd.formats import filterbank as fbm
+    from pypulsar_amd.formats import sigproc
+    C = x_tc.shape[1]
+    foff = -300.0 / C if foff is None else foff
+    params, hdr = sigproc.make_header(C, nbits, DT, 1550.0 + foff / 2, foff,
+                                      src_raj=123456.789, src_dej=-123456.5)
+    fn = str(tmp_path / name)
+    fbm.write_filterbank(fn, params, hdr, x_tc)
+    return fn
+
+
+@pytest.mark.parametrize("dtype", [np.uint8, np.uint16, np.float32])
+def test_zero_dm_filter_cli(gpu, tmp_path, dtype):
+    from pypulsar_amd.bin import zero_dm_filter as z
+    from pypulsar_amd.formats import filterbank as fbm
+    rng = np.random.default_rng(3)
+    nbits = {np.uint8: 8, np.uint16: 16, np.float32: 32}[dtype]
+    if dtype == np.float32:
+        x = rng.normal(0, 5, (5000, 40)).astype(dtype)
+    else:
+        x = rng.integers(0, np.iinfo(dtype).max, (5000, 40)).astype(dtype)
+    fn = _fil(tmp_path, x, nbits)
+    out = str(tmp_path / "out.fil")
+    assert z.main(["-o", out, fn]) == 0
+    fb = fbm.filterbank(out)
+    got = fb.read_all_samples().reshape(-1, 40)
+    want = orc.zero_dm_block(x)
+    assert got.dtype == dtype and got.shape == x.shape
+    if dtype == np.float32:
+        assert rel_err(got, want) <= 1e-5
+    else:
+        np.testing.assert_array_equal(got, want)
+    assert fb.header_params == fbm.filterbank(fn).header_params
+
+
+@pytest.mark.parametrize("foff_sign", [-1, 1])
+@pytest.mark.parametrize("all_samples", [False, True])
+def test_mockspec_cli(gpu, tmp_path, foff_sign, all_samples):
+    from pypulsar_amd.bin import mockspecfil2subbands as m
+    C, N = 24, 3 * 4096 + 1000
+    x = u8_data(C, N, 9).T.copy()  # [N, C]
+    fn = _fil(tmp_path, x, foff=foff_sign * 2.0)
+    outname = str(tmp_path / "sb")
+    args = ["-o", outname, fn] + (["--all-samples"] if all_samples else [])
+    assert m.main(args) == 0
+    nw = N if all_samples else (N // 4096 - 1) * 4096 + N % 4096
+    for k in range(C):
+        j = k if foff_sign > 0 else C - 1 - k  # reversed numbering when foff < 0
+        got = np.fromfile("%s.sub%04d" % (outname, k), dtype=np.uint8)
+        np.testing.assert_array_equal(got, x[:nw, j])
+    inf = open(outname + ".sub.inf").read()
+    assert "Number of bins in the time series      =  %d" % N in inf
+    assert "12:34:56.789" in inf and "-12:34:56.5" in inf
+    assert "Number of channels                     =  %d" % C in inf
+
+
+def test_waterfaller_cli(gpu, tmp_path):
+    from pypulsar_amd.bin import waterfaller as w
+    C, N = 64, 8000
+    x = u8_data(C, N, 13)
+    fn = _fil(tmp_path, x.T.copy())
+    png = str(tmp_path / "wf.png")
+    assert w.main(["-T", "0.01", "-n", "3000", "-d", "150", "--subdm", "150", "-s", "16",
+                   "--downsamp", "2", "--width-bins", "3", "--sweep-dm", "150",
+                   "--outfile", png, fn]) == 0
+    assert os.path.getsize(png) > 1000
+    # the device pipeline equals the oracle composition of waterfaller.py:103-127
+    from pypulsar_amd.formats import filterbank as fbm
+    opts = type("O", (), dict(dm=150.0, start=0.01, duration=None, nbins=3000, maskfile=None,
+                              width_bins=3, downsamp=2, nsub=16, subdm=150.0, scaleindep=False))
+    data = w.run(fn, opts)
+    fb = fbm.filterbank(fn)
+    start = int(np.round(0.01 / DT))
+    nb = 3000 + int(np.round(orc.delay_from_DM(150.0, fb.freqs.min()) / DT))
+    d = x[:, start:start + nb].astype(np.float64)
+    d, f = orc.subband(d, fb.freqs, DT, 16, 150.0, padval="mean")
+    d, _ = orc.dedisperse(d, f, DT, 150.0, padval="mean", trim=True)
+    d, _ = orc.downsample(d, DT, 2)
+    d = orc.smooth(orc.scaled(d), 3, "mean")
+    assert data.data.shape == d.shape
+    assert rel_err(data.data, d) <= 1e-5
