@@ -73,7 +73,7 @@ def test_mockspec_cli(gpu, tmp_path, foff_sign, all_samples):
 
 def test_waterfaller_cli(gpu, tmp_path):
     from pypulsar_amd.bin import waterfaller as w
-    C, N = 64, 8000
+    C, N = 64, 12000  # 3000 bins + the 150 pc/cc sweep (6201 bins at 1250 MHz)
     x = u8_data(C, N, 13)
     fn = _fil(tmp_path, x.T.copy())
     png = str(tmp_path / "wf.png")
