@@ -96,6 +96,16 @@ int pdd_downsample(const float* x, int64_t C, int64_t N, int64_t ld, int64_t fac
 int pdd_zero_dm(const void* in, int dtype, int64_t nspec, int64_t nchan, int64_t ld,
                 int layout, void* out, int64_t ld_out, void* stream);
 
+/* Streaming prologue, one HBM pass over a time-major block [nspec][nchan]
+ * (filterbank order, u8/u16/f32): corner turn + zero-DM in float mode
+ * (zero_dm != 0: every spectrum minus its float64 channel mean, the
+ * subtraction of bin/zero_dm_filter.py:30-39 without the integer cast) +
+ * Spectra.downsample(factor) (formats/spectra.py:329-351; factor divides 64):
+ *   out[c][j] = sum_{k<factor} (x[j*factor+k][c] - mean[j*factor+k]),
+ * j < nspec / factor, out channel-major float32. */
+int pdd_zdm_downsample(const void* in, int dtype, int64_t nspec, int64_t nchan, int64_t ld,
+                       int64_t factor, int zero_dm, float* out, int64_t ld_out, void* stream);
+
 /* ---- waterfaller post-chain (Spectra.scaled / scaled2 / masked / smooth) ---- */
 /* Whole-array statistics of x[C][N] into out4 (device float[4]):
  * {mean, population std, min, max}, float64 accumulation.

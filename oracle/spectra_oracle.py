@@ -303,3 +303,19 @@ def smooth(data, width=1, padval=0):
             tosmooth[width:-width] = chan
         chan[:] = np.convolve(tosmooth, kernel, "same")[width:-width]
     return out
+
+
+# --------------------------------------------------------------------------
+# streaming pipeline (new; SURVEY.md §8(d) config 5): zero-DM in float mode
+# (bin/zero_dm_filter.py:35 mean, without the integer cast) + downsample
+# (formats/spectra.py:329-351) of a time-major block
+# --------------------------------------------------------------------------
+
+
+def zdm_downsample(block_tc, factor, zero_dm=True):
+    """[nspec, nchan] time-major block -> [nchan, nspec // factor] float64."""
+    x = np.asarray(block_tc, dtype=np.float64)
+    if zero_dm:
+        x = x - x.mean(axis=1, keepdims=True)
+    n = (x.shape[0] // factor) * factor
+    return x[:n].reshape(n // factor, factor, x.shape[1]).sum(axis=1).T

@@ -485,6 +485,55 @@ __global__ __launch_bounds__(256) void k_smooth(const float* __restrict__ x, int
   }
 }
 
+// ---------------------------------------------------------------- streaming prologue
+// Per-spectrum channel mean (float64) of a time-major block.
+template <typename T>
+__global__ __launch_bounds__(256) void k_spectrum_mean(const T* __restrict__ in, int64_t nspec,
+                                                       int64_t nchan, int64_t ld,
+                                                       double* __restrict__ mean) {
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (s >= nspec) return;
+  const T* row = in + s * ld;
+  double acc = 0.0;
+  for (int64_t c = lane; c < nchan; c += 64) acc += (double)row[c];
+  acc = wave_sum(acc);
+  if (lane == 0) mean[s] = acc / (double)nchan;
+}
+
+// Fused corner turn + zero-DM (float mode) + downsample:
+//   out[c][j] = sum_{k < f} (x[j*f + k][c] - mean[j*f + k]),   mean = 0 if !mean
+// through a 64-spectrum x 64-channel LDS tile (f divides 64).
+template <typename T>
+__global__ __launch_bounds__(256) void k_zdm_ds(const T* __restrict__ in, int64_t nspec,
+                                                int64_t nchan, int64_t ld,
+                                                const double* __restrict__ mean, int f,
+                                                float* __restrict__ out, int64_t ld_out,
+                                                int64_t tiles_c) {
+  __shared__ float tile[64][65];
+  const int64_t tt = blockIdx.x / tiles_c, tc = blockIdx.x % tiles_c;
+  const int64_t t0 = tt * 64, c0 = tc * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t t = t0 + i, c = c0 + tx;
+    float v = 0.f;
+    if (t < nspec && c < nchan) v = (float)((double)in[t * ld + c] - (mean ? mean[t] : 0.0));
+    tile[i][tx] = v;
+  }
+  __syncthreads();
+  const int per = 64 / f;  // outputs per channel in this tile
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t c = c0 + i;
+    if (c >= nchan || tx >= per) continue;
+    const int64_t j = t0 / f + tx;
+    if ((j + 1) * f > nspec) continue;  // trailing partial group dropped (downsample trim)
+    float acc = 0.f;
+    for (int k = 0; k < f; ++k) acc += tile[tx * f + k][i];
+    out[c * ld_out + j] = acc;
+  }
+}
+
 static int grid_1d(int64_t n, int per_block = 256) {
   int64_t g = cdiv(n, per_block);
   if (g > 2048 * 8) g = 2048 * 8;
@@ -724,6 +773,39 @@ int pdd_smooth(const float* x, int64_t C, int64_t N, int64_t ld, int64_t width, 
   k_smooth<<<(unsigned)(C * tiles), 256, 0, as_stream(stream)>>>(x, N, ld, width, pad_mode, padvals,
                                                                  out, ld_out, tiles);
   PDD_LAUNCHED();
+  return 0;
+}
+
+int pdd_zdm_downsample(const void* in, int dtype, int64_t nspec, int64_t nchan, int64_t ld,
+                       int64_t factor, int zero_dm, float* out, int64_t ld_out, void* stream) {
+  PDD_REQUIRE(in && out, "pdd_zdm_downsample: null pointer");
+  PDD_REQUIRE(nspec >= 0 && nchan > 0 && ld >= nchan, "pdd_zdm_downsample: bad shape");
+  PDD_REQUIRE(factor >= 1 && factor <= 64 && 64 % factor == 0,
+              "pdd_zdm_downsample: factor must divide 64");
+  PDD_REQUIRE(ld_out >= nspec / factor, "pdd_zdm_downsample: ld_out too small");
+  if (nspec < factor) return 0;
+  hipStream_t s = as_stream(stream);
+  double* mean = nullptr;
+  if (zero_dm) PDD_HIP(hipMallocAsync((void**)&mean, (size_t)nspec * sizeof(double), s));
+  const int64_t tiles_c = cdiv(nchan, 64);
+  const int64_t blocks = cdiv(nspec, 64) * tiles_c;
+  PDD_REQUIRE(blocks < (1ll << 31), "pdd_zdm_downsample: too large");
+#define ZD(T)                                                                                   \
+  do {                                                                                          \
+    if (zero_dm)                                                                                \
+      k_spectrum_mean<T><<<(unsigned)cdiv(nspec, 4), 256, 0, s>>>((const T*)in, nspec, nchan, ld, \
+                                                                   mean);                       \
+    k_zdm_ds<T><<<(unsigned)blocks, 256, 0, s>>>((const T*)in, nspec, nchan, ld, mean,          \
+                                                 (int)factor, out, ld_out, tiles_c);            \
+  } while (0)
+  if (dtype == PDD_U8) ZD(uint8_t);
+  else if (dtype == PDD_U16) ZD(uint16_t);
+  else if (dtype == PDD_F32) ZD(float);
+  else PDD_REQUIRE(false, "pdd_zdm_downsample: bad dtype %d", dtype);
+#undef ZD
+  const hipError_t e = hipGetLastError();
+  if (mean) (void)hipFreeAsync(mean, s);
+  PDD_REQUIRE(e == hipSuccess, "pdd_zdm_downsample: launch failed: %s", hipGetErrorString(e));
   return 0;
 }
 

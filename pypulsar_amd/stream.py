@@ -1,0 +1,120 @@
+"""Streaming FRB-style pipeline (BASELINE.json configs[4]; SURVEY.md §8(d)
+config 5): continuous filterbank blocks -> zero-DM (float mode) -> downsample
+-> batched DM sweep, with pinned-host H2D copies overlapped with compute.
+
+Per input chunk (``block`` spectra of the stream, time-major [n, nchan] in
+file order, 8/16-bit or float32):
+
+    copy stream : pinned host chunk i --H2D--> raw[i % 2][0:n]
+    compute     : raw[(i-1) % 2][block : block + ov] <- raw[i % 2][0 : ov]   (D2D)
+                  pdd_zdm_downsample(raw[(i-1) % 2])  -> [C, (block + ov)/ds] f32
+                  DMSweep (interleave + sweep, trim)   -> plane [D, block/ds]
+
+``ov = max_bin * ds`` input spectra (the largest dispersion delay of the grid
+at the downsampled rate) of chunk i are appended to block i-1, so the
+concatenated per-block planes are exactly -- bit for bit -- the plane of the
+one-shot ``zero_dm -> downsample -> sweep(trim=True)`` over the whole stream
+(zero-DM is per spectrum, downsampling groups stay aligned because
+block % ds == 0, and every plane column sees all of its inputs).
+
+The H2D of chunk i+1 runs on its own HIP stream while block i is processed;
+the two raw buffers alternate, guarded by events.  No CPU fallback.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_ptr
+from .sweep import DMSweep
+
+_CODES = {torch.uint8: _lib.U8, torch.int16: _lib.U16, torch.float32: _lib.F32}
+
+
+class StreamingSweep(object):
+    """``StreamingSweep(dms, freqs, dt)(chunks)`` yields ``(t0, plane)``:
+    plane columns t0 .. t0 + plane.shape[1] - 1 of the stream's DM-time plane
+    (downsampled time index)."""
+
+    def __init__(self, dms, freqs, dt, block=1 << 18, downsamp=2, zero_dm=True,
+                 dtype=torch.uint8, device="cuda"):
+        _lib.require_gpu()
+        assert block % downsamp == 0 and 64 % downsamp == 0
+        self.freqs = np.asarray(freqs, dtype=np.float64)
+        self.C = len(self.freqs)
+        self.ds = int(downsamp)
+        self.dt = dt
+        self.zero_dm = bool(zero_dm)
+        self.dtype = dtype
+        self.device = torch.device(device)
+        self.sweep = DMSweep(dms, self.freqs, dt * self.ds, dtype="f32")
+        self.D = self.sweep.D
+        self.max_bin = max(0, self.sweep.max_bin)
+        self.block = int(block)
+        self.ov = self.max_bin * self.ds
+        assert self.ov <= self.block, "block must hold the overlap (max delay x downsamp)"
+        n_raw = self.block + self.ov
+        self.raw = [torch.empty((n_raw, self.C), dtype=dtype, device=self.device) for _ in range(2)]
+        self.f32 = torch.empty((self.C, n_raw // self.ds), dtype=torch.float32, device=self.device)
+        self.copy_stream = torch.cuda.Stream(device=self.device)
+        self.h2d = [torch.cuda.Event() for _ in range(2)]
+        self.free = [torch.cuda.Event() for _ in range(2)]
+        for e in self.free:
+            e.record(torch.cuda.current_stream(self.device))
+
+    @property
+    def n_out_block(self):
+        return self.block // self.ds
+
+    def _process(self, raw, n_valid, out=None):
+        """zero-DM + downsample + sweep of raw[:n_valid] -> plane (trim=True)."""
+        nd = n_valid // self.ds
+        n_out = max(0, nd - self.max_bin)
+        if out is None:
+            out = torch.empty((self.D, max(n_out, 0)), dtype=torch.float32, device=self.device)
+        if n_out == 0:
+            return out[:, :0]
+        call("pdd_zdm_downsample", ptr(raw), _CODES[self.dtype], n_valid, self.C, raw.stride(0),
+             self.ds, int(self.zero_dm), ptr(self.f32), self.f32.stride(0), stream_ptr())
+        self.sweep(self.f32[:, :nd], trim=True, out=out)
+        return out[:, :n_out]
+
+    def __call__(self, chunks, planes=None):
+        """chunks: iterable of host tensors [n, C] (pinned for an asynchronous
+        copy; every chunk but the last must hold exactly ``block`` spectra).
+        planes: optional list of two preallocated [D, block/ds] device planes
+        (reused alternately).  Yields (t0, plane)."""
+        cur = torch.cuda.current_stream(self.device)
+        prev = None  # (buffer index, n spectra)
+        t0 = 0
+        i = -1
+        for i, chunk in enumerate(chunks):
+            b = i % 2
+            n = chunk.shape[0]
+            assert chunk.shape[1] == self.C and n <= self.block
+            self.copy_stream.wait_event(self.free[b])
+            with torch.cuda.stream(self.copy_stream):
+                self.raw[b][:n].copy_(chunk, non_blocking=True)
+            self.h2d[b].record(self.copy_stream)
+            if prev is not None:
+                pb, pn = prev
+                assert pn == self.block, "only the last chunk may be short"
+                cur.wait_event(self.h2d[b])
+                take = min(self.ov, n)
+                if take:
+                    self.raw[pb][pn:pn + take].copy_(self.raw[b][:take])
+                out = None if planes is None else planes[pb]
+                plane = self._process(self.raw[pb], pn + take, out)
+                self.free[pb].record(cur)
+                yield t0, plane
+                t0 += plane.shape[1]
+            prev = (b, n)
+        if prev is not None:
+            pb, pn = prev
+            cur.wait_event(self.h2d[pb])
+            out = None if planes is None else planes[pb]
+            plane = self._process(self.raw[pb], pn, out)
+            self.free[pb].record(cur)
+            yield t0, plane
+
+    def close(self):
+        self.sweep.close()
