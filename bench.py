@@ -41,6 +41,10 @@ CONFIGS = {
     # north-star single-GPU target (4096 ch x 2048 DM x 2^22)
     "northstar": dict(C=4096, N=1 << 22, D=2048, dm_lo=0.0, dm_hi=1000.0),
     "small": dict(C=256, N=1 << 18, D=256, dm_lo=0.0, dm_hi=500.0),
+    # BASELINE.json configs[4]: streaming u8 blocks, zero-DM + ds 2 + 2048 DMs
+    "stream": dict(C=4096, N=1 << 18, D=2048, dm_lo=0.0, dm_hi=1000.0, ds=2),
+    # BASELINE.json configs[2]: two-stage subband sweep over a DDplan2b grid
+    "subband": dict(C=4096, N=1 << 20, nsub=64, dm_lo=0.0, dm_hi=1000.0, res=0.5),
 }
 
 
@@ -97,6 +101,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="config2", choices=sorted(CONFIGS))
+    ap.add_argument("--block", type=int, default=None, help="stream: spectra per block")
     ap.add_argument("--dtype", default="f32", choices=["f32", "u8"])
     ap.add_argument("--mode", default="timeblock", choices=["timeblock", "dmshard"])
     ap.add_argument("--cpu-trials", type=int, default=3)
@@ -120,6 +125,10 @@ def main():
     from pypulsar_amd.sweep import DMSweep
 
     cfg = CONFIGS[args.config]
+    if args.config == "stream":
+        return stream_bench(args, cfg, rank, world, dev)
+    if args.config == "subband":
+        return subband_bench(args, cfg, rank, world, dev)
     C, N, D = cfg["C"], cfg["N"], cfg["D"]
     dt = 64e-6
     freqs = band(C)
@@ -218,6 +227,151 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _finish(args, world, line):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(json.dumps(line))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def stream_bench(args, cfg, rank, world, dev):
+    """BASELINE configs[4]: continuous 8-bit blocks [block, C] from PINNED host
+    memory -> async H2D (copy stream) -> fused zero-DM (float) + downsample 2
+    -> 2048-DM sweep (pypulsar_amd.stream).  One step = one block through the
+    whole pipeline, H2D included.  Each rank streams its own data (weak)."""
+    from pypulsar_amd.stream import StreamingSweep
+    C, D, ds = cfg["C"], cfg["D"], cfg["ds"]
+    block = args.block or cfg["N"]
+    dt = 64e-6
+    freqs = band(C)
+    dms = np.linspace(cfg["dm_lo"], cfg["dm_hi"], D)
+    st = StreamingSweep(dms, freqs, dt, block=block, downsamp=ds)
+    # two distinct pinned chunks, reused cyclically (content is irrelevant to speed)
+    chunks = []
+    for i in range(2):
+        x = synth_block(block, C, 2000 + 10 * rank + i, "u8", dev)
+        h = torch.empty((block, C), dtype=torch.uint8, pin_memory=True)
+        h.copy_(x)
+        chunks.append(h)
+    del x
+    torch.cuda.synchronize()
+    nb = st.n_out_block
+    planes = [torch.empty((D, nb), dtype=torch.float32, device=dev) for _ in range(2)]
+    total = args.warmup + args.steps + 1  # +1: a block is emitted when the next chunk arrives
+    gen = st((chunks[i % 2] for i in range(total)), planes=planes)
+    done = 0
+    t0 = None
+    for _, plane in gen:
+        done += 1
+        if done == args.warmup:
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+        if done == args.warmup + args.steps:
+            break
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    units = D * nb * C * args.steps * world
+    value = units / el
+    ms = el / args.steps * 1e3
+    in_rate = block * args.steps * world / el  # input spectra per second
+    line = {
+        "metric": "DM-trial samples*channels/sec (node) + % HBM roofline",
+        "value": value, "unit": "samples*channels*DM/s (downsampled samples)",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic uint8 clip(round(N(128,16))) blocks in pinned host memory",
+        "config": {"workload": "streaming: %d-ch u8 blocks of %d spectra (pinned H2D, async) + "
+                               "zero-DM (float) + downsample %d + %d-DM sweep (0-%g pc/cc)"
+                               % (C, block, ds, D, cfg["dm_hi"]),
+                   "config_name": "stream", "channels": C, "block": block, "overlap": st.ov,
+                   "downsamp": ds, "dm_trials": D, "parallelism": "tb%d" % world},
+        "realtime_factor": (block * dt) / (ms * 1e-3),
+        "input_spectra_per_s": in_rate,
+        "roofline": {"bound": "mfma", "achieved": D * nb * C / (ms * 1e-3) / 1e12,
+                     "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+                     "frac": D * nb * C / (ms * 1e-3) / 1e12 / PEAK_F32_TFLOPS, "traffic": None,
+                     "note": "whole-step time (H2D, prologue, sweep) per block; one FP32 add "
+                             "per unit"},
+        "cpu_baseline": None,
+    }
+    st.close()
+    _finish(args, world, line)
+
+
+def subband_bench(args, cfg, rank, world, dev):
+    """BASELINE configs[2]: two-stage subband dedispersion over the DDplan2b
+    grid (Observation(64us, 1400, 300, 4096).gen_ddplan(0, 1000, 64, 0.5)):
+    per DDstep downsample, per subband pass subband(64, subDM), then the
+    pass's DM sweep (pypulsar_amd.sweep.execute_plan).  Work units are the
+    equivalent brute-force samples*channels*DM of the plan's trials."""
+    from pypulsar_amd.formats.spectra import Spectra
+    from pypulsar_amd.sweep import execute_plan
+    from pypulsar_amd.utils.ddplan import Observation
+    C, N = cfg["C"], cfg["N"]
+    dt = 64e-6
+    freqs = band(C)
+    plan = Observation(dt, 1400.0, 300.0, C).gen_ddplan(cfg["dm_lo"], cfg["dm_hi"], cfg["nsub"],
+                                                       cfg["res"])
+    x = synth_block(C, N, 3000 + rank, "u8", dev)
+    s = Spectra(freqs, dt, x)
+    units = 0
+    for step in plan.DDsteps:
+        n_ds = N // step.downsamp
+        from pypulsar_amd.delays import sweep_table
+        mb = int(max(0, sweep_table(step.DMs[-1:], freqs, dt * step.downsamp).max()))
+        units += len(step.DMs) * (n_ds - mb) * C
+
+    def one():
+        return execute_plan(s, plan, padval=0, trim=True)
+
+    for _ in range(args.warmup):
+        one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ms = el / args.steps * 1e3
+    line = {
+        "metric": "DM-trial samples*channels/sec (node) + % HBM roofline",
+        "value": units * args.steps * world / el,
+        "unit": "samples*channels*DM/s (brute-force-equivalent)",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic uint8 clip(round(N(128,16))) filterbank, generated on device",
+        "config": {"workload": "two-stage subband sweep %d ch -> %d subbands, DDplan2b "
+                               "(0-%g pc/cc, res %g ms): %s" % (C, cfg["nsub"], cfg["dm_hi"],
+                                                               cfg["res"],
+                                                               [(len(st.DMs), st.downsamp,
+                                                                 st.numprepsub)
+                                                                for st in plan.DDsteps]),
+                   "config_name": "subband", "channels": C, "samples": N,
+                   "dm_trials": int(sum(len(st.DMs) for st in plan.DDsteps)),
+                   "parallelism": "tb%d" % world},
+        "roofline": None,
+        "cpu_baseline": None,
+    }
+    _finish(args, world, line)
 
 
 if __name__ == "__main__":
