@@ -150,6 +150,12 @@ int pdd_sweep_execute(const pdd_sweep_plan* plan, const void* x, int64_t N, int6
  * DMs per block, time samples per block, LDS bytes per workgroup. */
 int pdd_sweep_plan_info(const pdd_sweep_plan* plan, int64_t* info /*[8]*/);
 int pdd_sweep_plan_destroy(pdd_sweep_plan* plan);
+/* Measurement hooks (bench.py): with timing on, pdd_sweep_execute brackets
+ * the sweep kernel(s) -- not the interleave pre-pass -- with HIP events on
+ * the execute stream; pdd_sweep_kernel_ms waits for and returns the last
+ * bracketed duration. */
+int pdd_sweep_set_timing(pdd_sweep_plan* plan, int on);
+int pdd_sweep_kernel_ms(pdd_sweep_plan* plan, float* ms);
 
 #ifdef __cplusplus
 }

@@ -1638,6 +1638,9 @@ struct pdd_sweep_plan {
   int max_bin = 0, min_bin = 0;
   int P = 0;               // ring kernel: prefetch distance (channels)
   int dtype = PDD_F32;     // input element type
+  hipEvent_t ev[2] = {nullptr, nullptr};  // timing of the sweep kernel (pdd_sweep_set_timing)
+  int timing = 0;
+  int timed = 0;           // launches bracketed since the last query
 };
 
 using namespace pdd;
@@ -1680,11 +1683,16 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
     const int64_t n_tblk = Qs / Tq;
     const int64_t blocks = n_tblk * p->n_dblk;
     if (blocks >= (1ll << 31)) { rc = -1; break; }
+    if (p->timing && t_base == 0) (void)hipEventRecord(p->ev[0], st);
     hipLaunchKernelGGL(il_kernel_for(p->v), dim3((unsigned)blocks), dim3(p->v.threads()),
                        p->lds_bytes, st, R, nR, (int)C, (int)lo, p->d_tab, out, ld_out,
                        (int)p->D, Qs, t_base, t_base + cnt, p->stride, (int)n_tblk,
                        (int)p->n_dblk, dbg);
     if (hipGetLastError() != hipSuccess) rc = -3;
+  }
+  if (p->timing) {
+    (void)hipEventRecord(p->ev[1], st);
+    const_cast<pdd_sweep_plan*>(p)->timed = 1;
   }
   (void)hipFreeAsync(R, st);
   if (rc == -1) set_error("pdd_sweep_execute: grid too large");
@@ -1896,8 +1904,30 @@ int pdd_sweep_execute(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
   return 0;
 }
 
+int pdd_sweep_set_timing(pdd_sweep_plan* p, int on) {
+  PDD_REQUIRE(p, "pdd_sweep_set_timing: null pointer");
+  if (on && !p->ev[0]) {
+    PDD_HIP(hipEventCreate(&p->ev[0]));
+    PDD_HIP(hipEventCreate(&p->ev[1]));
+  }
+  p->timing = on ? 1 : 0;
+  p->timed = 0;
+  return 0;
+}
+
+int pdd_sweep_kernel_ms(pdd_sweep_plan* p, float* ms) {
+  PDD_REQUIRE(p && ms, "pdd_sweep_kernel_ms: null pointer");
+  PDD_REQUIRE(p->timing && p->timed, "pdd_sweep_kernel_ms: no timed launch (pdd_sweep_set_timing)");
+  PDD_HIP(hipEventSynchronize(p->ev[1]));
+  PDD_HIP(hipEventElapsedTime(ms, p->ev[0], p->ev[1]));
+  p->timed = 0;
+  return 0;
+}
+
 int pdd_sweep_plan_destroy(pdd_sweep_plan* p) {
   if (!p) return 0;
+  if (p->ev[0]) (void)hipEventDestroy(p->ev[0]);
+  if (p->ev[1]) (void)hipEventDestroy(p->ev[1]);
   if (p->d_tab) (void)hipFree(p->d_tab);
   if (p->d_bmin) (void)hipFree(p->d_bmin);
   if (p->d_bspan) (void)hipFree(p->d_bspan);

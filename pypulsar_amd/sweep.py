@@ -113,6 +113,20 @@ class DMSweep(object):
              ptr(out), out.stride(0), n_out, stream_ptr(stream))
         return out
 
+    def set_timing(self, on=True, code=None):
+        """Bracket the sweep kernel of every execute with HIP events (on the
+        execute stream); read the last duration with kernel_ms()."""
+        code = (_lib.U8 if self.dtype == "u8" else _lib.F32) if code is None else code
+        _lib.check(_lib.lib().pdd_sweep_set_timing(self._plan(code), int(bool(on))),
+                   "pdd_sweep_set_timing")
+        self._timed_code = code
+
+    def kernel_ms(self):
+        v = ctypes.c_float()
+        _lib.check(_lib.lib().pdd_sweep_kernel_ms(self._plan(self._timed_code), ctypes.byref(v)),
+                   "pdd_sweep_kernel_ms")
+        return float(v.value)
+
     def close(self):
         for p in self._plans.values():
             _lib.lib().pdd_sweep_plan_destroy(p)

@@ -9,9 +9,12 @@ mkdir -p $O
 BA="--steps 5 --warmup 2 --no-cpu-baseline"
 python -c "import __graft_entry__ as g; g.build()" > $O/build.log 2>&1 \
  && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && echo SMOKE_OK \
- && timeout -k 10 900 python -m pytest tests -m gpu -q > $O/pytest_gpu.log 2>&1 && echo PYTEST_OK \
+ && timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 && echo PYTEST_OK \
  && timeout -k 10 600 python bench.py > $O/bench_f32.json 2> $O/bench_f32.err && echo BENCH_F32_OK \
  && timeout -k 10 300 python bench.py --dtype u8 --no-cpu-baseline > $O/bench_u8.json 2> $O/bench_u8.err && echo BENCH_U8_OK \
+ && timeout -k 10 300 python bench.py --config stream --steps 6 --warmup 2 > $O/bench_stream.json 2> $O/bench_stream.err && echo BENCH_STREAM_OK \
+ && timeout -k 10 300 python bench.py --config subband --steps 3 --warmup 1 > $O/bench_subband.json 2> $O/bench_subband.err && echo BENCH_SUBBAND_OK \
+ && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_stream -o kt --output-format csv -- python bench.py --config stream --steps 4 --warmup 1 > $O/kt_stream.log 2>&1 \
  && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_f32 -o kt --output-format csv -- python bench.py $BA > $O/kt_f32.log 2>&1 \
  && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_u8 -o kt --output-format csv -- python bench.py $BA --dtype u8 > $O/kt_u8.log 2>&1 \
  && timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_f32 -o p --output-format csv -- python bench.py $BA > $O/pmc1.log 2>&1 \
@@ -21,5 +24,5 @@ python -c "import __graft_entry__ as g; g.build()" > $O/build.log 2>&1 \
  && echo PROFILE_OK
 rc=$?
 tail -3 $O/pytest_gpu.log
-cat $O/bench_f32.json $O/bench_u8.json 2>/dev/null | cut -c1-400
+cat $O/bench_f32.json $O/bench_u8.json $O/bench_stream.json $O/bench_subband.json 2>/dev/null | cut -c1-300
 exit $rc
