@@ -1288,6 +1288,50 @@ __host__ __device__ constexpr int il_meta_bytes(int nlw, int nbuf, int cc, int d
   return nlw * il_mr(nbuf) * il_slot(cc, db) * 4;
 }
 
+// Tile order of k_sweep_il.  Blocks b and b+8 share an XCD (and its L2).
+// XCD x owns the time tiles [x*TX, (x+1)*TX), TX = n_tblk / 8, and walks them
+// in 2-D groups of GT time tiles x GJ trial blocks: at one channel the
+// concurrent windows of such a group overlap along both axes (a trial block's
+// window extends its neighbour's by the span, a time tile's by Tq), so the
+// group re-reads each staged element ~GT*GJ*(Tq+S)/(GT*Tq + GJ*S) times from
+// L2.  Leftover time tiles (n_tblk % 8) follow in natural order.
+// dbg bit 4: plain XCD-contiguous order (trial block fastest); bit 5: natural.
+__device__ __forceinline__ void il_tile_of(int bid, int n_tblk, int n_dblk, int dbg, int& dblk,
+                                           int& tblk) {
+  constexpr int GT = 8, GJ = 4;
+  const int total = n_tblk * n_dblk;
+  if (dbg & 32) {
+    dblk = bid % n_dblk;
+    tblk = bid / n_dblk;
+    return;
+  }
+  if (dbg & 16) {
+    const int full = (total / 8) * 8;
+    const int L = bid >= full ? bid : (bid % 8) * (total / 8) + bid / 8;
+    dblk = L % n_dblk;
+    tblk = L / n_dblk;
+    return;
+  }
+  const int TX = n_tblk / 8;
+  const int owned = 8 * TX * n_dblk;
+  if (bid >= owned) {
+    const int L = bid - owned;
+    dblk = L % n_dblk;
+    tblk = 8 * TX + L / n_dblk;
+    return;
+  }
+  const int x = bid % 8, k = bid / 8;  // k-th tile of XCD x
+  const int band = k / (GT * n_dblk);
+  const int gtb = min(GT, TX - band * GT);  // time tiles in this band
+  int r = k - band * GT * n_dblk;
+  const int nj = (n_dblk + GJ - 1) / GJ;
+  const int jg = min(r / (gtb * GJ), nj - 1);
+  const int gj = min(GJ, n_dblk - jg * GJ);  // trial blocks in this group
+  r -= jg * gtb * GJ;
+  dblk = jg * GJ + r % gj;
+  tblk = x * TX + band * GT + r / gj;
+}
+
 template <int G, int DPW, int NCW, int NLW, int CC, int NBUF>
 __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const float4* __restrict__ R, int64_t nR, int C, int lo, const int* __restrict__ mt,
@@ -1305,14 +1349,8 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   const int buf_e = CC * stride;
   int* metar = reinterpret_cast<int*>(img + NBUF * buf_e);  // [NLW][MR][SLOT]
 
-  // XCD-aware order: the n_dblk trial blocks of one time tile run back to
-  // back on one XCD (blocks b and b+8 share an XCD) and share its L2.
-  // dbg bit 4: chip-wide time-major order instead.
-  const int total = n_tblk * n_dblk;
-  const int full = (total / 8) * 8;
-  const int bid = blockIdx.x;
-  const int L = ((dbg & 16) || bid >= full) ? bid : (bid % 8) * (total / 8) + bid / 8;
-  const int dblk = L % n_dblk, tblk = L / n_dblk;
+  int dblk, tblk;
+  il_tile_of(blockIdx.x, n_tblk, n_dblk, dbg, dblk, tblk);
   const int64_t t0 = (int64_t)tblk * Tq;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
