@@ -263,7 +263,7 @@ def stream_bench(args, cfg, rank, world, dev):
     del x
     torch.cuda.synchronize()
     nb = st.n_out_block
-    planes = [torch.empty((D, nb), dtype=torch.float32, device=dev) for _ in range(2)]
+    planes = [torch.empty((D, nb), dtype=torch.float32, device=dev) for _ in range(3)]
     total = args.warmup + args.steps + 1  # +1: a block is emitted when the next chunk arrives
     gen = st((chunks[i % 2] for i in range(total)), planes=planes)
     done = 0

@@ -5,9 +5,10 @@ config 5): continuous filterbank blocks -> zero-DM (float mode) -> downsample
 Per input chunk (``block`` spectra of the stream, time-major [n, nchan] in
 file order, 8/16-bit or float32):
 
-    copy stream : pinned host chunk i --H2D--> raw[i % 2][0:n]
-    compute     : raw[(i-1) % 2][block : block + ov] <- raw[i % 2][0 : ov]   (D2D)
-                  pdd_zdm_downsample(raw[(i-1) % 2])  -> [C, (block + ov)/ds] f32
+    copy stream : pinned chunk i --H2D--> raw[i % 3][0:ov]      (head, event)
+                  pinned chunk i --H2D--> raw[i % 3][ov:n]     (rest, event)
+    compute     : raw[(i-1) % 3][block : block + ov] <- raw[i % 3][0 : ov]   (D2D)
+                  pdd_zdm_downsample(raw[(i-1) % 3])  -> [C, (block + ov)/ds] f32
                   DMSweep (interleave + sweep, trim)   -> plane [D, block/ds]
 
 ``ov = max_bin * ds`` input spectra (the largest dispersion delay of the grid
@@ -17,8 +18,10 @@ one-shot ``zero_dm -> downsample -> sweep(trim=True)`` over the whole stream
 (zero-DM is per spectrum, downsampling groups stay aligned because
 block % ds == 0, and every plane column sees all of its inputs).
 
-The H2D of chunk i+1 runs on its own HIP stream while block i is processed;
-the two raw buffers alternate, guarded by events.  No CPU fallback.
+Block i-1 waits only for the HEAD of chunk i (its overlap), so the rest of
+chunk i's H2D runs on the copy stream while block i-1 is processed; three raw
+buffers rotate so the next chunk's copy never waits for the block being
+computed.  Events guard every hand-off.  No CPU fallback.
 """
 import numpy as np
 import torch
@@ -53,11 +56,14 @@ class StreamingSweep(object):
         self.ov = self.max_bin * self.ds
         assert self.ov <= self.block, "block must hold the overlap (max delay x downsamp)"
         n_raw = self.block + self.ov
-        self.raw = [torch.empty((n_raw, self.C), dtype=dtype, device=self.device) for _ in range(2)]
+        self.nbuf = 3
+        self.raw = [torch.empty((n_raw, self.C), dtype=dtype, device=self.device)
+                    for _ in range(self.nbuf)]
         self.f32 = torch.empty((self.C, n_raw // self.ds), dtype=torch.float32, device=self.device)
         self.copy_stream = torch.cuda.Stream(device=self.device)
-        self.h2d = [torch.cuda.Event() for _ in range(2)]
-        self.free = [torch.cuda.Event() for _ in range(2)]
+        self.h2d_head = [torch.cuda.Event() for _ in range(self.nbuf)]
+        self.h2d = [torch.cuda.Event() for _ in range(self.nbuf)]
+        self.free = [torch.cuda.Event() for _ in range(self.nbuf)]
         for e in self.free:
             e.record(torch.cuda.current_stream(self.device))
 
@@ -81,29 +87,34 @@ class StreamingSweep(object):
     def __call__(self, chunks, planes=None):
         """chunks: iterable of host tensors [n, C] (pinned for an asynchronous
         copy; every chunk but the last must hold exactly ``block`` spectra).
-        planes: optional list of two preallocated [D, block/ds] device planes
-        (reused alternately).  Yields (t0, plane)."""
+        planes: optional list of preallocated [D, block/ds] device planes,
+        used in rotation.  Yields (t0, plane)."""
         cur = torch.cuda.current_stream(self.device)
         prev = None  # (buffer index, n spectra)
         t0 = 0
         i = -1
         for i, chunk in enumerate(chunks):
-            b = i % 2
+            b = i % self.nbuf
             n = chunk.shape[0]
             assert chunk.shape[1] == self.C and n <= self.block
+            head = min(self.ov, n)
             self.copy_stream.wait_event(self.free[b])
             with torch.cuda.stream(self.copy_stream):
-                self.raw[b][:n].copy_(chunk, non_blocking=True)
+                if head:
+                    self.raw[b][:head].copy_(chunk[:head], non_blocking=True)
+                self.h2d_head[b].record(self.copy_stream)
+                if n > head:
+                    self.raw[b][head:n].copy_(chunk[head:], non_blocking=True)
             self.h2d[b].record(self.copy_stream)
             if prev is not None:
                 pb, pn = prev
                 assert pn == self.block, "only the last chunk may be short"
-                cur.wait_event(self.h2d[b])
-                take = min(self.ov, n)
-                if take:
-                    self.raw[pb][pn:pn + take].copy_(self.raw[b][:take])
-                out = None if planes is None else planes[pb]
-                plane = self._process(self.raw[pb], pn + take, out)
+                cur.wait_event(self.h2d[pb])       # the block's own chunk
+                cur.wait_event(self.h2d_head[b])   # the next chunk's first ov spectra
+                if head:
+                    self.raw[pb][pn:pn + head].copy_(self.raw[b][:head])
+                out = None if planes is None else planes[pb % len(planes)]
+                plane = self._process(self.raw[pb], pn + head, out)
                 self.free[pb].record(cur)
                 yield t0, plane
                 t0 += plane.shape[1]
@@ -111,7 +122,7 @@ class StreamingSweep(object):
         if prev is not None:
             pb, pn = prev
             cur.wait_event(self.h2d[pb])
-            out = None if planes is None else planes[pb]
+            out = None if planes is None else planes[pb % len(planes)]
             plane = self._process(self.raw[pb], pn, out)
             self.free[pb].record(cur)
             yield t0, plane
