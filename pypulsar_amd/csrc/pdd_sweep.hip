@@ -1247,6 +1247,31 @@ __global__ __launch_bounds__(256) void k_interleave(const InT* __restrict__ x, i
   R[(int64_t)c * nR + j] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
+// u16 eighths for 8-bit data: R[c][j] = 8 samples X(c, b + j + k*Qs), k < 8,
+// as packed u16 pairs (word h = sample 2h | sample 2h+1 << 16); pads (integer
+// values 0..255, checked by the caller) and rotation baked in as for float32.
+__global__ __launch_bounds__(256) void k_interleave_u16(const uint8_t* __restrict__ x, int64_t ld,
+                                                        int64_t N, int64_t base, int64_t Qs,
+                                                        int64_t nR, int pad_mode,
+                                                        const float* __restrict__ padvals,
+                                                        uint4* __restrict__ R) {
+  const int c = blockIdx.y;
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= nR) return;
+  const uint8_t* row = x + (int64_t)c * ld;
+  const uint32_t pv = (pad_mode == PDD_PAD_VALUE) ? (uint32_t)padvals[c] : 0u;
+  uint32_t v[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t s = base + j + k * Qs;
+    if (s >= 0 && s < N) v[k] = row[s];
+    else if (pad_mode == PDD_PAD_ROTATE) v[k] = row[wrap_mod(s, N)];
+    else v[k] = pv;
+  }
+  R[(int64_t)c * nR + j] = make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16),
+                                      v[6] | (v[7] << 16));
+}
+
 // n DMAs of 64 elements (1 KiB) each, q = first, first + step, ...
 __device__ __forceinline__ int stage_il_dma(uint32_t lds_dst, const float4* src, int ne, int first,
                                             int step, int lane) {
@@ -1332,7 +1357,7 @@ __device__ __forceinline__ void il_tile_of(int bid, int n_tblk, int n_dblk, int 
   tblk = x * TX + band * GT + r / gj;
 }
 
-template <int G, int DPW, int NCW, int NLW, int CC, int NBUF>
+template <int G, int DPW, int NCW, int NLW, int CC, int NBUF, bool U16 = false>
 __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const float4* __restrict__ R, int64_t nR, int C, int lo, const int* __restrict__ mt,
     float* __restrict__ out, int64_t ld_out, int D, int64_t Qs, int64_t t_base, int64_t n_out,
@@ -1342,7 +1367,8 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   constexpr int ROW = DB + 4;
   constexpr int SLOT = il_slot(CC, DB);
   constexpr int MA = il_ma(NBUF), MR = il_mr(NBUF);
-  static_assert(DPW == 4 && G == 4, "b128 shift reads; one trial = 4 groups");
+  constexpr int S = U16 ? 8 : 4;  // samples per 16-byte element (quarters / eighths)
+  static_assert(DPW == 4 && G == (U16 ? 2 : 4), "b128 shift reads; one trial = 4 (f32) or 2 (u16) groups");
   static_assert(NBUF >= 2 && MA >= 2 * NBUF - 2 && MR > MA, "ring geometry");
   extern __shared__ __attribute__((aligned(16))) float smf[];
   uint4* img = reinterpret_cast<uint4*>(smf);
@@ -1434,17 +1460,48 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   }
 
   // ---------------- compute waves: ds_read_b128 at the trial's shift + adds
-  float acc[DPW][G][4];
+  // float32 elements: 4 quarter samples per read, float accumulators.
+  // u16 elements (8-bit data): 8 eighth samples per read as packed u16 pairs,
+  // accumulated with plain 32-bit adds (two u16 lanes per add, no carry while
+  // <= 257 channels of values <= 255 are summed) and flushed to float every
+  // 256 channels -- exact.
+  float acc[DPW][G][S];
 #pragma unroll
   for (int j = 0; j < DPW; ++j)
 #pragma unroll
     for (int g = 0; g < G; ++g)
 #pragma unroll
-      for (int k2 = 0; k2 < 4; ++k2) acc[j][g][k2] = 0.f;
+      for (int k2 = 0; k2 < S; ++k2) acc[j][g][k2] = 0.f;
+  uint32_t a16[U16 ? DPW : 1][U16 ? G : 1][4];
+  if constexpr (U16) {
+#pragma unroll
+    for (int j = 0; j < DPW; ++j)
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int h = 0; h < 4; ++h) a16[j][g][h] = 0u;
+  }
+  auto flush16 = [&]() {
+    if constexpr (U16) {
+#pragma unroll
+      for (int j = 0; j < DPW; ++j)
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            acc[j][g][2 * h] += (float)(a16[j][g][h] & 0xffffu);
+            acc[j][g][2 * h + 1] += (float)(a16[j][g][h] >> 16);
+            a16[j][g][h] = 0u;
+          }
+    }
+  };
+  int since_flush = 0;
   const uint32_t lane_byte = lds_addr_of(img) + lane * 16;
   const uint32_t meta_base = lds_addr_of(metar) + w * DPW * 4;  // loader 0's ring
   typedef int i32x4_t __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(3))) i32x4_t lds_i32x4_t;
+  typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) u32x4_t lds_u32x4_t;
   uint64_t ts_poll = 0, ts_comp = 0, tA = 0, tB = 0;
   __builtin_amdgcn_s_barrier();  // prologue barrier (metadata landed)
   asm volatile("" ::: "memory");
@@ -1468,31 +1525,61 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
             *(const lds_i32x4_t*)(uintptr_t)(meta_base + (uint32_t)((slot * SLOT + i * ROW) * 4));
         const uint32_t cb = lane_byte + (uint32_t)((b * CC + i) * stride * 16);
         const int ov[4] = {o.x, o.y, o.z, o.w};
-        f32x4_t v[DPW][G];
+        if constexpr (U16) {
+          // two trials at a time (a full scheduling barrier between the
+          // halves keeps the live read registers within the 128-VGPR budget)
 #pragma unroll
-        for (int j = 0; j < DPW; ++j)
+          for (int jh = 0; jh < DPW; jh += 2) {
+            u32x4_t v[2][G];
 #pragma unroll
-          for (int g2 = 0; g2 < G; ++g2)
-            v[j][g2] = *(const lds_f32x4_t*)(uintptr_t)(cb + (uint32_t)(ov[j] * 16) + g2 * 1024);
+            for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int j = 0; j < DPW; ++j)
+              for (int g2 = 0; g2 < G; ++g2)
+                v[j][g2] =
+                    *(const lds_u32x4_t*)(uintptr_t)(cb + (uint32_t)(ov[jh + j] * 16) + g2 * 1024);
 #pragma unroll
-          for (int g2 = 0; g2 < G; ++g2) {
-            acc[j][g2][0] += v[j][g2].x;
-            acc[j][g2][1] += v[j][g2].y;
-            acc[j][g2][2] += v[j][g2].z;
-            acc[j][g2][3] += v[j][g2].w;
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int g2 = 0; g2 < G; ++g2) {
+                a16[jh + j][g2][0] += v[j][g2].x;
+                a16[jh + j][g2][1] += v[j][g2].y;
+                a16[jh + j][g2][2] += v[j][g2].z;
+                a16[jh + j][g2][3] += v[j][g2].w;
+              }
+            __builtin_amdgcn_sched_barrier(0);
           }
-        __builtin_amdgcn_sched_group_barrier(0x100, 2 * G, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 4 * G, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, G, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 4 * G, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, G, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 4 * G, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 4 * G, 0);
+          if (++since_flush == 256) {
+            since_flush = 0;
+            flush16();
+          }
+        } else {
+          f32x4_t v[DPW][G];
+#pragma unroll
+          for (int j = 0; j < DPW; ++j)
+#pragma unroll
+            for (int g2 = 0; g2 < G; ++g2)
+              v[j][g2] = *(const lds_f32x4_t*)(uintptr_t)(cb + (uint32_t)(ov[j] * 16) + g2 * 1024);
+#pragma unroll
+          for (int j = 0; j < DPW; ++j)
+#pragma unroll
+            for (int g2 = 0; g2 < G; ++g2) {
+              acc[j][g2][0] += v[j][g2].x;
+              acc[j][g2][1] += v[j][g2].y;
+              acc[j][g2][2] += v[j][g2].z;
+              acc[j][g2][3] += v[j][g2].w;
+            }
+          __builtin_amdgcn_sched_group_barrier(0x100, 2 * G, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 4 * G, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, G, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 4 * G, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, G, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 4 * G, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 4 * G, 0);
+        }
       }
     }
   }
+  flush16();
   if (stamps) ts_comp += __builtin_amdgcn_s_memtime() - tB;
   if (stamps) {
     if (lane == 0) {
@@ -1508,7 +1595,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     if (d >= D) continue;
     float* orow = out + (int64_t)d * ld_out + t_base;
 #pragma unroll
-    for (int k2 = 0; k2 < 4; ++k2)
+    for (int k2 = 0; k2 < S; ++k2)
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const int64_t t = t0 + g * 64 + lane;
@@ -1559,7 +1646,7 @@ struct Variant {
   int ws;    // > 0: k_sweep_ws with this many dedicated loader waves (NW = compute waves)
   int il;    // 1: interleaved production path (k_interleave + k_sweep_il, ws loader waves)
   int threads() const { return (NW + ws) * 64; }
-  int elem_bytes() const { return u8 ? 2 * S : 4 * S; }
+  int elem_bytes() const { return il ? 16 : (u8 ? 2 * S : 4 * S); }  // il: 16-byte elements
   int Q() const { return 64 * G; }
   int TB() const { return lin && S == 2 ? 128 * G : S * 64 * G; }
   int DB() const { return NW * DPW; }
@@ -1588,7 +1675,8 @@ static const Variant kF32Variants[] = {{false, 4, 4, 4, 14, 2, 4, false, 0, 2, 1
                                        {false, 4, 4, 4, 8, 2, 3, true, 0},
                                        {false, 4, 4, 1, 8, 1, 2, false, 0},
                                        {false, 4, 1, 1, 1, 1, 2, false, 0}};
-static const Variant kU8Variants[] = {{false, 4, 4, 4, 14, 2, 4, false, 0, 2, 1},
+static const Variant kU8Variants[] = {{false, 8, 2, 4, 14, 2, 4, false, 0, 2, 1},
+                                      {false, 4, 4, 4, 14, 2, 4, false, 0, 2, 1},
                                       {true, 8, 2, 4, 8, 4, 2, false},
                                       {true, 8, 2, 4, 8, 2, 2, false},
                                       {true, 8, 2, 1, 8, 1, 2, false},
@@ -1605,8 +1693,11 @@ typedef void (*sweep_il_fn)(const float4*, int64_t, int, int, const int*, float*
                             int64_t, int64_t, int64_t, int, int, int, int);
 static sweep_il_fn il_kernel_for(const Variant& v) {
 #define IL(NCW_, NLW_, CC_, NB_)                                                             \
-  if (v.NW == NCW_ && v.ws == NLW_ && v.CC == CC_ && v.NBUF == NB_ && v.G == 4 && v.DPW == 4) \
+  if (v.S == 4 && v.NW == NCW_ && v.ws == NLW_ && v.CC == CC_ && v.NBUF == NB_ && v.G == 4 &&  \
+      v.DPW == 4)                                                                              \
     return k_sweep_il<4, 4, NCW_, NLW_, CC_, NB_>;
+  if (v.S == 8 && v.NW == 14 && v.ws == 2 && v.CC == 2 && v.NBUF == 4 && v.G == 2 && v.DPW == 4)
+    return k_sweep_il<2, 4, 14, 2, 2, 4, true>;
   IL(14, 2, 1, 8)
   IL(14, 2, 2, 4)
   IL(8, 2, 1, 6)
@@ -1689,17 +1780,20 @@ using namespace pdd;
 static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t ld, int pad_mode,
                       const float* padvals, float* out, int64_t ld_out, int64_t n_out,
                       void* stream) {
-  constexpr int Tq = 256;
+  const int Tq = 64 * p->v.G;
+  const int SP = p->v.S;  // samples per element: 4 (float32 quarters) or 8 (u16 eighths)
+  const bool u16 = (SP == 8);
+  PDD_REQUIRE(!u16 || p->dtype == PDD_U8, "pdd_sweep_execute: u16 path needs 8-bit input");
   const int64_t C = p->C;
   const int64_t lo = std::min(0, p->min_bin), hi = std::max(0, p->max_bin);
   int64_t budget = (int64_t)8 << 30;  // bytes of R per segment
   if (const char* e = getenv("PDD_SWEEP_SEG_BYTES")) budget = std::max<int64_t>(atoll(e), 1 << 16);
   const int64_t nr_max = budget / (C * 16);
-  int64_t seg = (nr_max - (hi - lo) - 64) / Tq * Tq * 4;  // output samples per segment
+  int64_t seg = (nr_max - (hi - lo) - 64) / Tq * Tq * SP;  // output samples per segment
   PDD_REQUIRE(seg > 0, "pdd_sweep_execute: delay span %lld too wide for the segment budget",
               (long long)(hi - lo));
-  seg = std::min(seg, cdiv(n_out, 4 * Tq) * 4 * Tq);
-  const int64_t qs_max = seg / 4;
+  seg = std::min(seg, cdiv(n_out, (int64_t)SP * Tq) * SP * Tq);
+  const int64_t qs_max = seg / SP;
   const int64_t nr_alloc = qs_max + (hi - lo) + 64;
   float4* R = nullptr;
   hipStream_t st = as_stream(stream);
@@ -1708,10 +1802,13 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
   int rc = 0;
   for (int64_t t_base = 0; t_base < n_out && rc == 0; t_base += seg) {
     const int64_t cnt = std::min(seg, n_out - t_base);
-    const int64_t Qs = cdiv(cdiv(cnt, 4), Tq) * Tq;
+    const int64_t Qs = cdiv(cdiv(cnt, SP), Tq) * Tq;
     const int64_t nR = Qs + (hi - lo) + 64;
     dim3 g1((unsigned)cdiv(nR, 256), (unsigned)C);
-    if (p->dtype == PDD_U8)
+    if (u16)
+      hipLaunchKernelGGL(k_interleave_u16, g1, dim3(256), 0, st, (const uint8_t*)x, ld, N,
+                         t_base + lo, Qs, nR, pad_mode, padvals, (uint4*)R);
+    else if (p->dtype == PDD_U8)
       hipLaunchKernelGGL(k_interleave<uint8_t>, g1, dim3(256), 0, st, (const uint8_t*)x, ld, N,
                          t_base + lo, Qs, nR, pad_mode, padvals, R);
     else
@@ -1747,7 +1844,7 @@ int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int d
               "pdd_sweep_plan_create: bad extents D=%lld C=%lld", (long long)D, (long long)C);
   PDD_REQUIRE(dtype == PDD_F32 || dtype == PDD_U8, "pdd_sweep_plan_create: dtype must be F32 or U8");
   const Variant* cands = dtype == PDD_U8 ? kU8Variants : kF32Variants;
-  const int ncand = dtype == PDD_U8 ? 5 : 13;
+  const int ncand = dtype == PDD_U8 ? 6 : 13;
 
   const int fv = forced_variant();
   for (int vi = (fv >= 0 && fv < ncand) ? fv : 0; vi < ncand; ++vi) {
