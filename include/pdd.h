@@ -146,6 +146,18 @@ int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int d
 int pdd_sweep_execute(const pdd_sweep_plan* plan, const void* x, int64_t N, int64_t ld,
                       int pad_mode, const float* padvals, float* out, int64_t ld_out,
                       int64_t n_out, void* stream);
+/* Grouped sweep: n_grp independent channel groups of C channels each
+ * (channels g*C .. g*C+C-1 of the input), every group with its own [D][C]
+ * table: host_table is [n_grp][D][C].  One launch replaces n_grp sweeps --
+ * the stage-1 subband passes of a DDplan step (Spectra.subband at each subDM,
+ * formats/spectra.py:96-138, one group per subband) or the stage-2 sweeps of
+ * its passes (one group per pass).  Trial d of group g is written to plane
+ * row g*row_g + d*row_d. */
+int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int64_t D, int64_t C,
+                                  int dtype, pdd_sweep_plan** plan);
+int pdd_sweep_execute_grouped(const pdd_sweep_plan* plan, const void* x, int64_t N, int64_t ld,
+                              int pad_mode, const float* padvals, float* out, int64_t ld_out,
+                              int64_t n_out, int64_t row_g, int64_t row_d, void* stream);
 /* Extents used by the plan (for DESIGN/bench reporting): DM trials, channels,
  * DMs per block, time samples per block, LDS bytes per workgroup. */
 int pdd_sweep_plan_info(const pdd_sweep_plan* plan, int64_t* info /*[8]*/);

@@ -27,6 +27,7 @@ EXPORTS = (
     "pdd_zero_dm", "pdd_sweep_plan_create", "pdd_sweep_execute", "pdd_sweep_plan_info",
     "pdd_sweep_plan_destroy", "pdd_global_stats", "pdd_scale_rows", "pdd_masked_fill",
     "pdd_smooth", "pdd_zdm_downsample", "pdd_sweep_set_timing", "pdd_sweep_kernel_ms",
+    "pdd_sweep_plan_create_grouped", "pdd_sweep_execute_grouped",
 )
 
 
@@ -63,6 +64,9 @@ _SIGS = {
     "pdd_smooth": ([_vp, _i64, _i64, _i64, _i64, _int, _vp, _vp, _i64, _vp], _int),
     "pdd_zdm_downsample": ([_vp, _int, _i64, _i64, _i64, _i64, _int, _vp, _i64, _vp], _int),
     "pdd_sweep_set_timing": ([_vp, _int], _int),
+    "pdd_sweep_plan_create_grouped": ([_vp, _i64, _i64, _i64, _int, ctypes.POINTER(_vp)], _int),
+    "pdd_sweep_execute_grouped": ([_vp, _vp, _i64, _i64, _int, _vp, _vp, _i64, _i64, _i64, _i64,
+                                   _vp], _int),
     "pdd_sweep_kernel_ms": ([_vp, ctypes.POINTER(ctypes.c_float)], _int),
 }
 

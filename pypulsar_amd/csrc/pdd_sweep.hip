@@ -1361,7 +1361,11 @@ template <int G, int DPW, int NCW, int NLW, int CC, int NBUF, bool U16 = false>
 __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const float4* __restrict__ R, int64_t nR, int C, int lo, const int* __restrict__ mt,
     float* __restrict__ out, int64_t ld_out, int D, int64_t Qs, int64_t t_base, int64_t n_out,
-    int stride, int n_tblk, int n_dblk, int dbg) {
+    int stride, int n_tblk, int n_dblk, int dbg, int64_t row_g, int64_t row_d) {
+  // Grouped sweeps: C is the channel count of ONE group; blockIdx.x / (tiles
+  // per group) is the group, whose channels are R rows [grp*C, grp*C + C),
+  // whose tables are mt[grp][...], and whose trial d lands in plane row
+  // grp*row_g + d*row_d (ungrouped: 0, 0, 1).
   constexpr int Tq = 64 * G;
   constexpr int DB = NCW * DPW;
   constexpr int ROW = DB + 4;
@@ -1376,11 +1380,14 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   int* metar = reinterpret_cast<int*>(img + NBUF * buf_e);  // [NLW][MR][SLOT]
 
   int dblk, tblk;
-  il_tile_of(blockIdx.x, n_tblk, n_dblk, dbg, dblk, tblk);
+  const int per_grp = n_tblk * n_dblk;
+  const int grp = blockIdx.x / per_grp;
+  il_tile_of(blockIdx.x - grp * per_grp, n_tblk, n_dblk, dbg, dblk, tblk);
+  R += (int64_t)grp * C * nR;
   const int64_t t0 = (int64_t)tblk * Tq;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int* mt_b = mt + (int64_t)dblk * C * ROW;
+  const int* mt_b = mt + ((int64_t)grp * n_dblk + dblk) * C * ROW;
   const int nchunk = (C + CC - 1) / CC;
   const bool stamps = (dbg & 4) != 0;  // dbg bit 2: per-wave cycle stamps into `out`
 
@@ -1593,7 +1600,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   for (int j = 0; j < DPW; ++j) {
     const int d = d0 + j;
     if (d >= D) continue;
-    float* orow = out + (int64_t)d * ld_out + t_base;
+    float* orow = out + ((int64_t)grp * row_g + (int64_t)d * row_d) * ld_out + t_base;
 #pragma unroll
     for (int k2 = 0; k2 < S; ++k2)
 #pragma unroll
@@ -1690,7 +1697,7 @@ static int64_t lds_budget(const Variant& v) {
 static constexpr int kLdsMax = 160 * 1024;
 
 typedef void (*sweep_il_fn)(const float4*, int64_t, int, int, const int*, float*, int64_t, int,
-                            int64_t, int64_t, int64_t, int, int, int, int);
+                            int64_t, int64_t, int64_t, int, int, int, int, int64_t, int64_t);
 static sweep_il_fn il_kernel_for(const Variant& v) {
 #define IL(NCW_, NLW_, CC_, NB_)                                                             \
   if (v.S == 4 && v.NW == NCW_ && v.ws == NLW_ && v.CC == CC_ && v.NBUF == NB_ && v.G == 4 &&  \
@@ -1767,6 +1774,7 @@ struct pdd_sweep_plan {
   int max_bin = 0, min_bin = 0;
   int P = 0;               // ring kernel: prefetch distance (channels)
   int dtype = PDD_F32;     // input element type
+  int64_t n_grp = 1;       // independent channel groups (grouped sweep)
   hipEvent_t ev[2] = {nullptr, nullptr};  // timing of the sweep kernel (pdd_sweep_set_timing)
   int timing = 0;
   int timed = 0;           // launches bracketed since the last query
@@ -1779,12 +1787,12 @@ using namespace pdd;
 // after the segment loop); each segment is one k_interleave + one k_sweep_il.
 static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t ld, int pad_mode,
                       const float* padvals, float* out, int64_t ld_out, int64_t n_out,
-                      void* stream) {
+                      int64_t row_g, int64_t row_d, void* stream) {
   const int Tq = 64 * p->v.G;
   const int SP = p->v.S;  // samples per element: 4 (float32 quarters) or 8 (u16 eighths)
   const bool u16 = (SP == 8);
   PDD_REQUIRE(!u16 || p->dtype == PDD_U8, "pdd_sweep_execute: u16 path needs 8-bit input");
-  const int64_t C = p->C;
+  const int64_t C = p->C * p->n_grp;  // all channels (groups are contiguous channel ranges)
   const int64_t lo = std::min(0, p->min_bin), hi = std::max(0, p->max_bin);
   int64_t budget = (int64_t)8 << 30;  // bytes of R per segment
   if (const char* e = getenv("PDD_SWEEP_SEG_BYTES")) budget = std::max<int64_t>(atoll(e), 1 << 16);
@@ -1816,13 +1824,13 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
                          t_base + lo, Qs, nR, pad_mode, padvals, R);
     if (hipGetLastError() != hipSuccess) { rc = -3; break; }
     const int64_t n_tblk = Qs / Tq;
-    const int64_t blocks = n_tblk * p->n_dblk;
+    const int64_t blocks = n_tblk * p->n_dblk * p->n_grp;
     if (blocks >= (1ll << 31)) { rc = -1; break; }
     if (p->timing && t_base == 0) (void)hipEventRecord(p->ev[0], st);
     hipLaunchKernelGGL(il_kernel_for(p->v), dim3((unsigned)blocks), dim3(p->v.threads()),
-                       p->lds_bytes, st, R, nR, (int)C, (int)lo, p->d_tab, out, ld_out,
+                       p->lds_bytes, st, R, nR, (int)p->C, (int)lo, p->d_tab, out, ld_out,
                        (int)p->D, Qs, t_base, t_base + cnt, p->stride, (int)n_tblk,
-                       (int)p->n_dblk, dbg);
+                       (int)p->n_dblk, dbg, row_g, row_d);
     if (hipGetLastError() != hipSuccess) rc = -3;
   }
   if (p->timing) {
@@ -1839,7 +1847,13 @@ extern "C" {
 
 int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int dtype,
                           pdd_sweep_plan** plan_out) {
+  return pdd_sweep_plan_create_grouped(host_table, 1, D, C, dtype, plan_out);
+}
+
+int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int64_t D, int64_t C,
+                                  int dtype, pdd_sweep_plan** plan_out) {
   PDD_REQUIRE(host_table && plan_out, "pdd_sweep_plan_create: null pointer");
+  PDD_REQUIRE(n_grp >= 1 && n_grp * C < (1 << 20), "pdd_sweep_plan_create: bad group count");
   PDD_REQUIRE(D > 0 && C > 0 && D < (1 << 24) && C < (1 << 20),
               "pdd_sweep_plan_create: bad extents D=%lld C=%lld", (long long)D, (long long)C);
   PDD_REQUIRE(dtype == PDD_F32 || dtype == PDD_U8, "pdd_sweep_plan_create: dtype must be F32 or U8");
@@ -1849,14 +1863,20 @@ int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int d
   const int fv = forced_variant();
   for (int vi = (fv >= 0 && fv < ncand) ? fv : 0; vi < ncand; ++vi) {
     const Variant v = cands[vi];
+    if (n_grp > 1 && !v.il) continue;  // only the interleaved kernel sweeps groups
     const int64_t DB = v.DB();
     const int64_t n_dblk = cdiv(D, DB);
     const int64_t Dpad = n_dblk * DB;
-    std::vector<int> tab((size_t)(C * Dpad));
-    std::vector<int> bmin((size_t)(n_dblk * C)), bspan((size_t)(n_dblk * C));
+    std::vector<int> mt_all;  // interleaved path: mt of every group, concatenated
     int max_span = 0, mx = INT32_MIN, mn = INT32_MAX;
+    std::vector<int> tab, bmin, bspan;
+    for (int64_t grp = 0; grp < n_grp; ++grp) {
+    const int32_t* htab = host_table + grp * D * C;
+    tab.assign((size_t)(C * Dpad), 0);
+    bmin.assign((size_t)(n_dblk * C), 0);
+    bspan.assign((size_t)(n_dblk * C), 0);
     for (int64_t d = 0; d < Dpad; ++d) {
-      const int32_t* row = host_table + std::min(d, D - 1) * C;
+      const int32_t* row = htab + std::min(d, D - 1) * C;
       for (int64_t c = 0; c < C; ++c) tab[(size_t)(c * Dpad + d)] = row[c];
     }
     for (int64_t b = 0; b < n_dblk; ++b) {
@@ -1878,6 +1898,20 @@ int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int d
     // kernel adds to its LDS base): rel[c][d] = table[d][c] - bmin[d / DB][c]
     for (int64_t c = 0; c < C; ++c)
       for (int64_t d = 0; d < Dpad; ++d) tab[(size_t)(c * Dpad + d)] -= bmin[(size_t)((d / DB) * C + c)];
+    if (v.il) {
+      // mt[grp][dblk][c][DB + 4] = shifts rel. to bmin, then {bmin, span, 0, 0}
+      const int64_t ROWN = DB + 4;
+      const size_t off = mt_all.size();
+      mt_all.resize(off + (size_t)(n_dblk * C * ROWN), 0);
+      for (int64_t b = 0; b < n_dblk; ++b)
+        for (int64_t c = 0; c < C; ++c) {
+          const size_t base = off + (size_t)((b * C + c) * ROWN);
+          for (int64_t d = 0; d < DB; ++d) mt_all[base + d] = tab[(size_t)(c * Dpad + b * DB + d)];
+          mt_all[base + DB] = bmin[(size_t)(b * C + c)];
+          mt_all[base + DB + 1] = bspan[(size_t)(b * C + c)];
+        }
+    }
+    }  // groups
     int ringP = 0;
     if (v.ring) {
       // rel = shift - bmin + ring offset; meta = {bmin, span, ring offset, 0}
@@ -1933,18 +1967,9 @@ int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int d
     p->lds_bytes = (int)need;
     p->P = ringP;
     p->dtype = dtype;
+    p->n_grp = n_grp;
     if (v.il) {
-      // mt[dblk][c][DB + 4] = shifts rel. to bmin, then {bmin, span, 0, 0}
-      const int64_t ROWN = DB + 4;
-      std::vector<int> mtv((size_t)(n_dblk * C * ROWN), 0);
-      for (int64_t b = 0; b < n_dblk; ++b)
-        for (int64_t c = 0; c < C; ++c) {
-          const size_t base = (size_t)((b * C + c) * ROWN);
-          for (int64_t d = 0; d < DB; ++d) mtv[base + d] = tab[(size_t)(c * Dpad + b * DB + d)];
-          mtv[base + DB] = bmin[(size_t)(b * C + c)];
-          mtv[base + DB + 1] = bspan[(size_t)(b * C + c)];
-        }
-      tab.swap(mtv);
+      tab.swap(mt_all);
     } else if (v.lin || v.ws) {
       // block-major layouts read by per-chunk metadata DMAs:
       //   rel [dblk][c][DB], meta[dblk][c] = {bmin, span}
@@ -2013,7 +2038,7 @@ int pdd_sweep_execute(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
   PDD_REQUIRE(pad_mode == PDD_PAD_ROTATE || (pad_mode == PDD_PAD_VALUE && padvals),
               "pdd_sweep_execute: bad pad mode %d", pad_mode);
   if (n_out == 0) return 0;
-  if (p->v.il) return execute_il(p, x, N, ld, pad_mode, padvals, out, ld_out, n_out, stream);
+  if (p->v.il) return execute_il(p, x, N, ld, pad_mode, padvals, out, ld_out, n_out, 0, 1, stream);
   // every staged index must stay inside int64 / the LDS image: the shifts are
   // bounded by the plan, the samples by N + n_out.
   const int64_t n_tblk = cdiv(n_out, p->v.TB());
@@ -2037,6 +2062,19 @@ int pdd_sweep_execute(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
                      p->stride, (int)n_tblk, (int)p->n_dblk);
   PDD_LAUNCHED();
   return 0;
+}
+
+int pdd_sweep_execute_grouped(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t ld,
+                              int pad_mode, const float* padvals, float* out, int64_t ld_out,
+                              int64_t n_out, int64_t row_g, int64_t row_d, void* stream) {
+  PDD_REQUIRE(p && x && out, "pdd_sweep_execute_grouped: null pointer");
+  PDD_REQUIRE(p->v.il, "pdd_sweep_execute_grouped: plan has no grouped kernel");
+  PDD_REQUIRE(N > 0 && ld >= N && n_out >= 0 && ld_out >= n_out && row_g >= 0 && row_d >= 0,
+              "pdd_sweep_execute_grouped: bad shape");
+  PDD_REQUIRE(pad_mode == PDD_PAD_ROTATE || (pad_mode == PDD_PAD_VALUE && padvals),
+              "pdd_sweep_execute_grouped: bad pad mode %d", pad_mode);
+  if (n_out == 0) return 0;
+  return execute_il(p, x, N, ld, pad_mode, padvals, out, ld_out, n_out, row_g, row_d, stream);
 }
 
 int pdd_sweep_set_timing(pdd_sweep_plan* p, int on) {

@@ -168,3 +168,102 @@ def execute_plan(spectra, ddplan, padval=0, trim=True):
             sw.close()
         results.append((step, outs))
     return results
+
+
+class GroupedSweep(object):
+    """One launch for ``n_grp`` independent sweeps over contiguous channel
+    groups: group g sweeps channels g*C .. g*C + C - 1 of the input with its
+    own [D][C] delay table; trial d of group g lands in plane row
+    g*row_g + d*row_d (pdd_sweep_plan_create_grouped / _execute_grouped)."""
+
+    def __init__(self, tables, dtype="f32"):
+        _lib.require_gpu()
+        t = np.ascontiguousarray(_delays.to_int32(np.asarray(tables)))
+        assert t.ndim == 3, "tables must be [n_grp, D, C]"
+        self.n_grp, self.D, self.C = t.shape
+        self.max_bin = int(t.max()) if t.size else 0
+        self.dtype = dtype
+        code = _lib.U8 if dtype == "u8" else _lib.F32
+        h = ctypes.c_void_p()
+        _lib.check(_lib.lib().pdd_sweep_plan_create_grouped(
+            t.ctypes.data_as(ctypes.c_void_p), self.n_grp, self.D, self.C, code, ctypes.byref(h)),
+            "pdd_sweep_plan_create_grouped")
+        self._plan = h
+
+    def __call__(self, x, n_out, out, row_g, row_d, pad_mode=_lib.PAD_VALUE, padvals=None,
+                 stream=None):
+        assert x.dim() == 2 and x.shape[0] == self.n_grp * self.C and x.stride(1) == 1
+        if pad_mode == _lib.PAD_VALUE and padvals is None:
+            padvals = torch.zeros(x.shape[0], dtype=torch.float32, device=x.device)
+        call("pdd_sweep_execute_grouped", self._plan, ptr(x), x.shape[1], x.stride(0), pad_mode,
+             ptr(padvals), ptr(out), out.stride(0), n_out, row_g, row_d, stream_ptr(stream))
+        return out
+
+    def close(self):
+        if self._plan is not None:
+            _lib.lib().pdd_sweep_plan_destroy(self._plan)
+            self._plan = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def execute_plan_grouped(spectra, ddplan, padval=0):
+    """Two-stage DDplan executor in TWO grouped launches per step (trim=True).
+
+    Per DDstep: downsample (Spectra.downsample semantics); with subbands,
+    stage 1 forms every pass's subbands at once -- a grouped sweep with one
+    group per subband (its C/nsub channels) whose trials are the passes'
+    subDMs (Spectra.subband shifts + group sum, spectra.py:96-138; pads as
+    there, full length) -- and stage 2 sweeps every pass's DMs at once -- one
+    group per pass, whose channels are that pass's subbands at their centre
+    frequencies (Spectra.dedisperse(dm, trim=True) + channel sum).  Without
+    subbands a step is one plain DMSweep.  Returns [(step, dms, plane)], plane
+    rows = the step's DMs, columns = the common prefix of the per-DM trimmed
+    series (N' - the step's largest delay)."""
+    import copy
+    from .formats.spectra import _pad_args
+    results = []
+    for step in ddplan.DDsteps:
+        base = copy.deepcopy(spectra)
+        if step.downsamp > 1:
+            base.downsample(step.downsamp)
+        calls = step.subband_calls()
+        if calls[0][0] is None:
+            sw = DMSweep(step.DMs, base.freqs, base.dt, cur_dm=base.dm,
+                         dtype="u8" if base._raw8 is not None else "f32")
+            results.append((step, step.DMs, sw(base, padval=padval, trim=True)))
+            sw.close()
+            continue
+        x = base.device_data
+        C, N = x.shape
+        nsub = step.numsub
+        cps = C // nsub
+        freqs = np.asarray(base.freqs, dtype=np.float64)
+        subdms = [c[0] for c in calls]
+        ncall = len(calls)
+        # stage 1: [nsub groups][ncall trials][cps channels]
+        t1 = np.stack([_delays.subband_bins(sd, freqs, base.dt, nsub, cur_dm=base.dm)
+                       for sd in subdms])                      # [ncall, C]
+        t1 = t1.reshape(ncall, nsub, cps).transpose(1, 0, 2)    # [nsub, ncall, cps]
+        g1 = GroupedSweep(t1, "f32")
+        mode, pv = _pad_args(x, padval)
+        sub = torch.empty((ncall * nsub, N), dtype=torch.float32, device=x.device)
+        g1(x, N, sub, row_g=1, row_d=nsub, pad_mode=mode, padvals=pv)
+        g1.close()
+        # stage 2: [ncall groups][per-call DMs][nsub subbands at their centres]
+        _, _, ctr = _delays.subband_layout(freqs, nsub)
+        per = len(calls[0][1])
+        assert all(len(c[1]) == per for c in calls)
+        t2 = np.stack([_delays.sweep_table(c[1], ctr, base.dt, cur_dm=base.dm) for c in calls])
+        g2 = GroupedSweep(t2, "f32")
+        n_out = max(0, N - max(0, g2.max_bin))
+        plane = torch.empty((ncall * per, max(n_out, 1)), dtype=torch.float32, device=x.device)
+        if n_out:
+            g2(sub, n_out, plane, row_g=per, row_d=1)
+        g2.close()
+        results.append((step, step.DMs, plane[:, :n_out]))
+    return results
