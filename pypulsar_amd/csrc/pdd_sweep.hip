@@ -1674,6 +1674,8 @@ static const Variant kF32Variants[] = {{false, 4, 4, 4, 14, 2, 4, false, 0, 2, 1
                                        {false, 4, 4, 4, 8, 1, 6, false, 0, 2, 1},
                                        {false, 4, 4, 4, 12, 1, 8, false, 0, 4, 1},
                                        {false, 4, 4, 4, 8, 2, 3, false, 0, 2, 1},
+                                       {false, 4, 4, 4, 8, 1, 3, false, 0, 2, 1},
+                                       {false, 4, 4, 4, 4, 1, 3, false, 0, 2, 1},
                                        {false, 4, 4, 4, 8, 2, 3, false, 0, 1},
                                        {false, 4, 4, 4, 8, 2, 3, false, 0, 2},
                                        {false, 4, 4, 4, 8, 2, 2, false, 0},
@@ -1684,6 +1686,8 @@ static const Variant kF32Variants[] = {{false, 4, 4, 4, 14, 2, 4, false, 0, 2, 1
                                        {false, 4, 1, 1, 1, 1, 2, false, 0}};
 static const Variant kU8Variants[] = {{false, 8, 2, 4, 14, 2, 4, false, 0, 2, 1},
                                       {false, 4, 4, 4, 14, 2, 4, false, 0, 2, 1},
+                                      {false, 4, 4, 4, 8, 1, 3, false, 0, 2, 1},
+                                      {false, 4, 4, 4, 4, 1, 3, false, 0, 2, 1},
                                       {true, 8, 2, 4, 8, 4, 2, false},
                                       {true, 8, 2, 4, 8, 2, 2, false},
                                       {true, 8, 2, 1, 8, 1, 2, false},
@@ -1710,6 +1714,8 @@ static sweep_il_fn il_kernel_for(const Variant& v) {
   IL(8, 2, 1, 6)
   IL(12, 4, 1, 8)
   IL(8, 2, 2, 3)
+  IL(8, 2, 1, 3)
+  IL(4, 2, 1, 3)
 #undef IL
   return nullptr;
 }
@@ -1858,7 +1864,7 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
               "pdd_sweep_plan_create: bad extents D=%lld C=%lld", (long long)D, (long long)C);
   PDD_REQUIRE(dtype == PDD_F32 || dtype == PDD_U8, "pdd_sweep_plan_create: dtype must be F32 or U8");
   const Variant* cands = dtype == PDD_U8 ? kU8Variants : kF32Variants;
-  const int ncand = dtype == PDD_U8 ? 6 : 13;
+  const int ncand = dtype == PDD_U8 ? 8 : 15;
 
   const int fv = forced_variant();
   for (int vi = (fv >= 0 && fv < ncand) ? fv : 0; vi < ncand; ++vi) {

@@ -21,7 +21,7 @@ def test_grouped_equals_individual(gpu):
     tables, planes = [], []
     for g in range(G):
         freqs = np.sort(rng.uniform(1200, 1600, C))[::-1]
-        dms = np.sort(rng.uniform(0, 120, 9))
+        dms = np.sort(rng.uniform(0, 40, 9))
         sw = DMSweep(dms, freqs, DT)
         tables.append(sw.table)
         planes.append(sw(x[g * C:(g + 1) * C], trim=False).cpu().numpy())
