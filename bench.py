@@ -316,11 +316,14 @@ def stream_bench(args, cfg, rank, world, dev):
 def subband_bench(args, cfg, rank, world, dev):
     """BASELINE configs[2]: two-stage subband dedispersion over the DDplan2b
     grid (Observation(64us, 1400, 300, 4096).gen_ddplan(0, 1000, 64, 0.5)):
-    per DDstep downsample, per subband pass subband(64, subDM), then the
-    pass's DM sweep (pypulsar_amd.sweep.execute_plan).  Work units are the
-    equivalent brute-force samples*channels*DM of the plan's trials."""
+    per DDstep downsample, then all 40 subband passes as ONE grouped sweep
+    (stage 1) and all passes' DM sweeps as ONE grouped sweep (stage 2)
+    (pypulsar_amd.sweep.execute_plan_grouped; equal to the per-pass
+    subband(64, subDM) + sweep executor, tests/test_gpu_grouped.py).  Work
+    units are the equivalent brute-force samples*channels*DM of the plan's
+    trials (the quantity the two-stage method replaces)."""
     from pypulsar_amd.formats.spectra import Spectra
-    from pypulsar_amd.sweep import execute_plan
+    from pypulsar_amd.sweep import execute_plan_grouped
     from pypulsar_amd.utils.ddplan import Observation
     C, N = cfg["C"], cfg["N"]
     dt = 64e-6
@@ -337,7 +340,7 @@ def subband_bench(args, cfg, rank, world, dev):
         units += len(step.DMs) * (n_ds - mb) * C
 
     def one():
-        return execute_plan(s, plan, padval=0, trim=True)
+        return execute_plan_grouped(s, plan, padval=0)
 
     for _ in range(args.warmup):
         one()

@@ -224,29 +224,36 @@ def execute_plan_grouped(spectra, ddplan, padval=0):
     subbands a step is one plain DMSweep.  Returns [(step, dms, plane)], plane
     rows = the step's DMs, columns = the common prefix of the per-DM trimmed
     series (N' - the step's largest delay)."""
-    import copy
     from .formats.spectra import _pad_args
     results = []
+    src = spectra.device_data
     for step in ddplan.DDsteps:
-        base = copy.deepcopy(spectra)
+        # downsampled view of the data (Spectra.downsample semantics, without
+        # copying or modifying the caller's Spectra)
+        dt = spectra.dt * step.downsamp
         if step.downsamp > 1:
-            base.downsample(step.downsamp)
+            C0, N0 = src.shape
+            n_ds = N0 // step.downsamp
+            x = torch.empty((C0, n_ds), dtype=torch.float32, device=src.device)
+            if n_ds:
+                call("pdd_downsample", ptr(src), C0, N0, src.stride(0), step.downsamp, ptr(x), n_ds,
+                     stream_ptr())
+        else:
+            x = src
         calls = step.subband_calls()
         if calls[0][0] is None:
-            sw = DMSweep(step.DMs, base.freqs, base.dt, cur_dm=base.dm,
-                         dtype="u8" if base._raw8 is not None else "f32")
-            results.append((step, step.DMs, sw(base, padval=padval, trim=True)))
+            sw = DMSweep(step.DMs, spectra.freqs, dt, cur_dm=spectra.dm, dtype="f32")
+            results.append((step, step.DMs, sw(x, padval=padval, trim=True)))
             sw.close()
             continue
-        x = base.device_data
         C, N = x.shape
         nsub = step.numsub
         cps = C // nsub
-        freqs = np.asarray(base.freqs, dtype=np.float64)
+        freqs = np.asarray(spectra.freqs, dtype=np.float64)
         subdms = [c[0] for c in calls]
         ncall = len(calls)
         # stage 1: [nsub groups][ncall trials][cps channels]
-        t1 = np.stack([_delays.subband_bins(sd, freqs, base.dt, nsub, cur_dm=base.dm)
+        t1 = np.stack([_delays.subband_bins(sd, freqs, dt, nsub, cur_dm=spectra.dm)
                        for sd in subdms])                      # [ncall, C]
         t1 = t1.reshape(ncall, nsub, cps).transpose(1, 0, 2)    # [nsub, ncall, cps]
         g1 = GroupedSweep(t1, "f32")
@@ -258,7 +265,7 @@ def execute_plan_grouped(spectra, ddplan, padval=0):
         _, _, ctr = _delays.subband_layout(freqs, nsub)
         per = len(calls[0][1])
         assert all(len(c[1]) == per for c in calls)
-        t2 = np.stack([_delays.sweep_table(c[1], ctr, base.dt, cur_dm=base.dm) for c in calls])
+        t2 = np.stack([_delays.sweep_table(c[1], ctr, dt, cur_dm=spectra.dm) for c in calls])
         g2 = GroupedSweep(t2, "f32")
         n_out = max(0, N - max(0, g2.max_bin))
         plane = torch.empty((ncall * per, max(n_out, 1)), dtype=torch.float32, device=x.device)
