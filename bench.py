@@ -80,10 +80,83 @@ def cpu_baseline(cfg, ntrials, dt):
         s = orc.channel_sum(d)
         work += s.shape[0] * C
     el = time.perf_counter() - t0
-    return dict(value=work / el, unit="samples*channels*DM/s", cores=1, kind="port",
-                sample="%d full-length DM trials (dedisperse(trim=True)+channel sum), "
-                       "%d ch x %d samples, float64 NumPy, 1 thread, %.1f s"
-                       % (ntrials, C, N, el))
+    res = dict(value=work / el, unit="samples*channels*DM/s", cores=1, kind="port",
+               sample="%d full-length DM trials (dedisperse(trim=True)+channel sum), "
+                      "%d ch x %d samples, float64 NumPy C-order, 1 thread, %.1f s"
+                      % (ntrials, C, N, el))
+    res["cpu_model"] = _cpu_model()
+    res["nproc"] = os.cpu_count()
+    res["f_order_1core"] = _cpu_forder(x, freqs, dt, pick[-1], orc)
+    res["all_cores"] = _cpu_pool(x, freqs, dt, dms, orc)
+    return res
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def _cpu_forder(x, freqs, dt, dm, orc, n=1 << 17):
+    """One trial on the F-order layout get_spectra produces (filterbank.py:
+    155-157 reshape + .T), where the reference's per-channel rotate walks
+    strided rows: first ``n`` samples only, per unit."""
+    n = min(n, x.shape[1])
+    xf = np.asfortranarray(x[:, :n])
+    t0 = time.perf_counter()
+    d, _ = orc.dedisperse(xf, freqs, dt, dm, padval=0, trim=True)
+    s = orc.channel_sum(d)
+    el = time.perf_counter() - t0
+    return dict(value=s.shape[0] * x.shape[0] / el, cores=1,
+                sample="1 DM trial (DM %.1f) on F-order %d ch x %d samples, %.1f s"
+                       % (dm, x.shape[0], n, el))
+
+
+_POOL_X = None
+
+
+def _pool_task(args):
+    """Reference algorithm on one channel block of one DM trial: the shifts are
+    per channel (spectra.py:54-94), so the channel sum of a trial is the sum of
+    its channel-block partial sums."""
+    from oracle import spectra_oracle as orc
+    c0, c1, bins, n_keep = args
+    sub = orc.shift_channels(_POOL_X[c0:c1].copy(), bins[c0:c1], padval=0)
+    sub[:, :n_keep].sum(axis=0)
+    return (c1 - c0) * n_keep
+
+
+def _cpu_pool(x, freqs, dt, dms, orc, workers=12, ntrials=16, cblk=32):
+    """DM-parallel multiprocessing variant: ``workers``
+    forked processes over (DM, 32-channel block) tasks of ``ntrials``
+    full-length trials.  12, not the box's 16-CPU share: the forked children
+    inherit the parent's GPU file descriptors and the box limits how many
+    processes may hold the card."""
+    import multiprocessing as mp
+    global _POOL_X
+    _POOL_X = x
+    C, N = x.shape
+    pick = dms[np.linspace(0, len(dms) - 1, ntrials).astype(int)]
+    tasks = []
+    for dm in pick:
+        bins = orc.dedisperse_bins(dm, 0.0, freqs, dt)
+        n_keep = N - max(0, int(bins.max()))
+        tasks += [(c, min(C, c + cblk), bins, n_keep) for c in range(0, C, cblk)]
+    workers = min(workers, len(tasks))
+    ctx = mp.get_context("fork")
+    with ctx.Pool(workers) as pool:
+        pool.map(_pool_task, tasks[:workers])  # fork + first touch, untimed
+        t0 = time.perf_counter()
+        work = sum(pool.map(_pool_task, tasks, chunksize=1))
+        el = time.perf_counter() - t0
+    _POOL_X = None
+    return dict(value=work / el, cores=workers,
+                sample="%d full-length DM trials split into %d-channel blocks over %d forked "
+                       "processes, float64 NumPy C-order, %.1f s" % (ntrials, cblk, workers, el))
 
 
 def load_pmc(path, key):

@@ -33,7 +33,7 @@ def per_kernel(pattern, counter):
 
 def main():
     os.makedirs(DST, exist_ok=True)
-    for name in ("f32", "u8", "stream"):
+    for name in ("f32", "u8", "stream", "subband"):
         f = glob.glob(os.path.join(SRC, "kt_" + name, "**", "*kernel_stats.csv"), recursive=True)
         if f:
             shutil.copy(f[0], os.path.join(DST, "%s_%s_kernel_stats.csv" % (TAG, name)))

@@ -15,6 +15,7 @@ python -c "import __graft_entry__ as g; g.build()" > $O/build.log 2>&1 \
  && timeout -k 10 300 python bench.py --config stream --steps 6 --warmup 2 > $O/bench_stream.json 2> $O/bench_stream.err && echo BENCH_STREAM_OK \
  && timeout -k 10 300 python bench.py --config subband --steps 3 --warmup 1 > $O/bench_subband.json 2> $O/bench_subband.err && echo BENCH_SUBBAND_OK \
  && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_stream -o kt --output-format csv -- python bench.py --config stream --steps 4 --warmup 1 > $O/kt_stream.log 2>&1 \
+ && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_subband -o kt --output-format csv -- python bench.py --config subband --steps 3 --warmup 1 --no-cpu-baseline > $O/kt_subband.log 2>&1 \
  && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_f32 -o kt --output-format csv -- python bench.py $BA > $O/kt_f32.log 2>&1 \
  && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_u8 -o kt --output-format csv -- python bench.py $BA --dtype u8 > $O/kt_u8.log 2>&1 \
  && timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_f32 -o p --output-format csv -- python bench.py $BA > $O/pmc1.log 2>&1 \
