@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 # MI355X peaks (MI355X_MICROARCH.md §Chip-level parameters)
 PEAK_HBM_GBS = 8000.0
 PEAK_F32_TFLOPS = 157.3   # FP32 vector peak == FP32 dense MFMA peak on gfx950
+PEAK_ADD_T = 78.6         # pure adds: 256 CU x 2.4 GHz x 128 (v_pk_add_f32), SURVEY.md §8(d)
 
 CONFIGS = {
     # BASELINE.json configs[1]
@@ -45,6 +46,8 @@ CONFIGS = {
     "stream": dict(C=4096, N=1 << 18, D=2048, dm_lo=0.0, dm_hi=1000.0, ds=2),
     # BASELINE.json configs[2]: two-stage subband sweep over a DDplan2b grid
     "subband": dict(C=4096, N=1 << 20, nsub=64, dm_lo=0.0, dm_hi=1000.0, res=0.5),
+    # single-pulse search over the config2 plane
+    "search": dict(C=1024, N=1 << 20, D=1024, dm_lo=0.0, dm_hi=1000.0),
 }
 
 
@@ -202,6 +205,8 @@ def main():
         return stream_bench(args, cfg, rank, world, dev)
     if args.config == "subband":
         return subband_bench(args, cfg, rank, world, dev)
+    if args.config == "search":
+        return search_bench(args, cfg, rank, world, dev)
     C, N, D = cfg["C"], cfg["N"], cfg["D"]
     dt = 64e-6
     freqs = band(C)
@@ -258,6 +263,9 @@ def main():
     s_in = 1 if args.dtype == "u8" else 4
     adds_per_launch = units_rank                 # one FP32 add per work unit
     achieved_tf = adds_per_launch / (kern_ms * 1e-3) / 1e12
+    # LDS roof: ds_read_b128 at 256 B/clk/CU feeds 4 f32 samples (f32 path)
+    # or 8 u16 samples (8-bit path) per 16 B -> T adds/s
+    lds_roof = 256 * 2.4e9 * 16 * (8 if args.dtype == "u8" else 4) / 1e12  # CUs x clk x reads/clk
     uniq_bytes = C * N * s_in + len(dms) * n_out * 4
     achieved_gbs = uniq_bytes / (kern_ms * 1e-3) / 1e9
     pmc_key = "%s_%s" % (args.config, args.dtype)
@@ -292,7 +300,10 @@ def main():
                          "kernel": "pdd::k_sweep_il", "kernel_ms": kern_ms,
                          "note": "compute roof: one FP32 add per samp*ch*DM; no MFMA-shaped "
                                  "work exists, the FP32 vector peak equals the FP32 dense MFMA "
-                                 "peak (157.3 TF) on gfx950; see DESIGN.md"},
+                                 "peak (157.3 TF) on gfx950; see DESIGN.md",
+                         # the roofs that actually bind an add-only, LDS-fed kernel
+                         "add_peak": PEAK_ADD_T, "frac_add_peak": achieved_tf / PEAK_ADD_T,
+                         "lds_roof": lds_roof, "frac_lds_roof": achieved_tf / lds_roof},
             "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": PEAK_HBM_GBS,
                              "unit": "GB/s", "frac": achieved_gbs / PEAK_HBM_GBS,
                              "bytes_per_launch": uniq_bytes},
@@ -312,6 +323,63 @@ def _finish(args, world, line):
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def search_bench(args, cfg, rank, world, dev):
+    """Single-pulse boxcar search (pypulsar_amd.search) of the config2 DM-time
+    plane (1024 DMs x 1,034,083 samples, f32, made once by the sweep, untimed).
+    One step = chunk statistics + boxcar search of the whole plane, 13 widths
+    1..150.  Both kernels read the plane once: algorithmic bytes per step =
+    2 x plane bytes (+ the per-chunk stats, <0.1%)."""
+    from pypulsar_amd.search import SinglePulseSearch
+    from pypulsar_amd.sweep import DMSweep
+    C, N, D = cfg["C"], cfg["N"], cfg["D"]
+    dt = 64e-6
+    dms = np.linspace(cfg["dm_lo"], cfg["dm_hi"], D)
+    sw = DMSweep(dms, band(C), dt, dtype="u8")
+    x = synth_block(C, N, 1234 + rank, "u8", dev)
+    plane = sw(x, trim=True)
+    del x
+    sps = SinglePulseSearch(threshold=6.0)
+    n = plane.shape[1]
+    for _ in range(args.warmup):
+        sps.raw(plane)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    t0 = time.perf_counter()
+    ev[0].record()
+    for _ in range(args.steps):
+        cands, count = sps.raw(plane)
+    ev[1].record()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ms = ev[0].elapsed_time(ev[1]) / args.steps
+    byts = 2 * D * n * 4
+    achieved = byts / (ms * 1e-3) / 1e9
+    line = {
+        "metric": "DM-time plane samples searched/sec (single-pulse boxcar search)",
+        "value": D * n * world * args.steps / el,
+        "unit": "plane samples/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "config2 sweep plane of a synthetic uint8 filterbank (generated on device)",
+        "config": {"workload": "boxcar search of a %d DM x %d sample plane, widths 1..150 (13), "
+                               "detrend chunks 1000, threshold 6" % (D, n),
+                   "candidates_last_step": int(count.item())},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS, "traffic": None,
+                     "kernel": "pdd::k_sp_stats + pdd::k_sp_search", "kernel_ms": ms,
+                     "bytes_per_step": byts},
+        "cpu_baseline": None,
+    }
+    return _finish(args, world, line)
 
 
 def stream_bench(args, cfg, rank, world, dev):

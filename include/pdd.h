@@ -169,6 +169,25 @@ int pdd_sweep_plan_destroy(pdd_sweep_plan* plan);
 int pdd_sweep_set_timing(pdd_sweep_plan* plan, int on);
 int pdd_sweep_kernel_ms(pdd_sweep_plan* plan, float* ms);
 
+/* ---- single-pulse boxcar search over a DM-time plane (SURVEY.md §8(f)
+ * rank 4; no reference search -- the boxcar is Pulse.smooth,
+ * formats/pulse.py:217-241; definition in pypulsar_amd/search.py).
+ * x: [D][n] float32 plane, row stride ld.  L: detrend chunk length. */
+/* Per row and chunk of L samples (last may be short): mean and 1/std
+ * (0 where std == 0), written to [D][ceil(n/L)] arrays. */
+int pdd_sp_chunk_stats(const float* x, int64_t D, int64_t n, int64_t ld, int64_t L, float* mean,
+                       float* istd, void* stream);
+/* Boxcar S/N of every start and width (widths: HOST array, ascending,
+ * 1..1025, at most 32) on the chunk-normalised rows; one candidate per
+ * (row, window of 1024 starts) with S/N >= threshold, appended to cands as
+ * int32 records {row, start, width, float-bits snr} through the device
+ * counter *count (incremented for every candidate, stored while
+ * < max_cands: the caller checks for overflow).  Record order is not
+ * deterministic; the set is. */
+int pdd_sp_search(const float* x, int64_t D, int64_t n, int64_t ld, int64_t L, const float* mean,
+                  const float* istd, const int32_t* widths, int n_widths, float threshold,
+                  int32_t* cands, int64_t max_cands, unsigned long long* count, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -98,3 +98,50 @@ def dm_sharded_sweep(x, shape, dtype, dms, freqs, dt, n_out, sweep_fn=None, src=
     else:
         part = torch.zeros((0, n_out), dtype=torch.float32, device=x.device)
     return gather_planes(part, slices, dst=dst, group=group)
+
+
+def gather_candidates(cands, group=None):
+    """All-gather per-rank candidate record arrays (small: 40 B each) and
+    merge them, sorted by (DM, sample), on every rank."""
+    from .search import merge
+    world = dist.get_world_size(group)
+    parts = [None] * world
+    dist.all_gather_object(parts, cands, group=group)
+    return merge(parts)
+
+
+def dm_sharded_search(x, shape, dtype, dms, freqs, dt, n_out, sweep_fn=None, search_fn=None,
+                      src=0, work=None, group=None, device=None, threshold=6.0):
+    """DM sharding with the search on the rank that swept: broadcast one block
+    from ``src``, sweep this rank's DM slice, search its plane locally and
+    exchange only the candidates -- the DM-time planes never leave their GPU
+    ("keep them resident per rank for a downstream search").
+    Every DM row is searched whole on one rank, so the merged list equals the
+    single-GPU search of the full plane.  ``search_fn(plane, dms_slice) ->
+    records`` defaults to the HIP SinglePulseSearch."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    slices = dm_slices(len(dms), world, work)
+    if rank != src:
+        x = torch.empty(shape, dtype=dtype, device=device)
+    broadcast_block(x, src=src, group=group)
+    lo, hi = slices[rank]
+    if sweep_fn is None:
+        from .sweep import DMSweep
+
+        def sweep_fn(blk, sub):
+            code = "u8" if blk.dtype == torch.uint8 else "f32"
+            sw = DMSweep(sub, freqs, dt, dtype=code)
+            out = torch.empty((len(sub), n_out), dtype=torch.float32, device=blk.device)
+            sw(blk, out=out)
+            return out
+    if search_fn is None:
+        from .search import SinglePulseSearch
+        sps = SinglePulseSearch(threshold=threshold)
+
+        def search_fn(plane, sub):
+            return sps(plane, sub, dt)
+    cands = None
+    if hi > lo:
+        cands = search_fn(sweep_fn(x, dms[lo:hi])[:, :n_out], dms[lo:hi])
+    return gather_candidates(cands, group=group)

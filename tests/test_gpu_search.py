@@ -1,0 +1,99 @@
+"""Single-pulse search (pdd_sp_chunk_stats + pdd_sp_search) on the GPU against
+the float64 oracle (oracle/search_oracle.py) and end to end behind the sweep.
+Tolerance: S/N within 1e-4 relative (f32 prefix sums vs float64); (start,
+width) bit-exact except where the oracle's best and runner-up are closer
+than 1e-4 (a float near-tie)."""
+import numpy as np
+import pytest
+
+from conftest import band, u8_data
+from oracle import search_oracle as so
+
+pytestmark = pytest.mark.gpu
+WIDTHS = (1, 2, 3, 4, 6, 9, 14, 20, 30, 45, 70, 100, 150)
+
+
+def _check(gpu_c, ora, margins, thr):
+    og = {(d, t // 1024): (t, w, s, m) for (d, t, w, s), m in zip(ora, margins)}
+    gg = {(int(r), int(t) // 1024): (int(t), int(w), float(s))
+          for r, t, w, s in zip(gpu_c["row"], gpu_c["Sample"], gpu_c["Downfact"], gpu_c["Sigma"])}
+    for k in set(og) | set(gg):
+        if k in og and k in gg:
+            t, w, s, m = og[k]
+            assert abs(gg[k][2] - s) <= 1e-4 * max(1.0, abs(s)), (k, gg[k], og[k])
+            if m > 1e-4 * abs(s):
+                assert gg[k][:2] == (t, w), (k, gg[k], og[k])
+        else:  # only allowed at the threshold
+            s = og[k][2] if k in og else gg[k][2]
+            assert abs(s - thr) <= 1e-4 * abs(thr), (k, s)
+
+
+@pytest.mark.parametrize("D,n,L", [(7, 5000, 1000), (3, 1024, 256), (2, 777, 1000),
+                                   (1, 100, 30), (4, 3 * 1024 + 1, 1024)])
+def test_search_vs_oracle(gpu, D, n, L):
+    import torch
+    from pypulsar_amd.search import SinglePulseSearch
+    rng = np.random.default_rng(D * 1000 + n)
+    x = rng.normal(0, 1, (D, n))
+    for d in range(D):  # a few pulses of random width
+        for _ in range(2):
+            w = int(rng.integers(1, 60))
+            t = int(rng.integers(0, max(1, n - w)))
+            x[d, t:t + w] += rng.uniform(0.5, 4.0)
+    x[0, n // 3:n // 3 + 3] += 8.0  # at least one clear detection
+    x = x.astype(np.float32)
+    thr = 4.0
+    sp = SinglePulseSearch(threshold=thr, widths=WIDTHS, detrendlen=L)
+    got = sp(torch.from_numpy(x).cuda(), dms=np.arange(D) * 1.0, dt=1e-3)
+    ora, margins = so.search(x.astype(np.float64), WIDTHS, thr, L)
+    assert len(ora) > 0
+    _check(got, ora, margins, thr)
+
+
+def test_search_strided_constant_and_overflow(gpu):
+    import torch
+    from pypulsar_amd.search import SinglePulseSearch
+    rng = np.random.default_rng(5)
+    big = torch.zeros((4, 3000), device="cuda")
+    big[:, :2500] = torch.from_numpy(rng.normal(0, 1, (4, 2500)).astype(np.float32)).cuda()
+    big[1, 600:610] += 5.0
+    big[2, :2500] = 7.0  # constant row: std 0 -> z 0 -> no candidate
+    view = big[:, :2500]  # row stride 3000
+    sp = SinglePulseSearch(threshold=5.0, detrendlen=500)
+    got = sp(view, dms=[1.0, 2.0, 3.0, 4.0], dt=1e-3, t0=10)
+    assert 2 not in set(got["row"])
+    hit = got[got["row"] == 1]
+    assert len(hit) == 1 and abs(int(hit["Sample"][0]) - 610) <= 10
+    ora, m = so.search(view.cpu().numpy().astype(np.float64), sp.widths, 5.0, 500)
+    got0 = got.copy()
+    got0["Sample"] -= 10
+    _check(got0, ora, m, 5.0)
+    small = SinglePulseSearch(threshold=-100.0, detrendlen=500, max_cands=3)
+    with pytest.raises(RuntimeError):
+        small(view, dms=[1.0, 2.0, 3.0, 4.0], dt=1e-3)
+
+
+def test_sweep_then_search_finds_dispersed_pulse(gpu):
+    """End to end: a dispersed pulse injected at DM 120 into an 8-bit
+    filterbank -> DMSweep plane -> search: the brightest candidate sits at the
+    injected DM (grid step 2) and arrival sample."""
+    import torch
+    from pypulsar_amd.delays import delay_from_DM
+    from pypulsar_amd.search import SinglePulseSearch
+    from pypulsar_amd.sweep import DMSweep
+    C, N, dt = 256, 1 << 15, 64e-6
+    freqs = band(C)
+    x = u8_data(C, N, 9).astype(np.int32)
+    dm0, t0, w = 120.0, 9000, 8
+    d = delay_from_DM(dm0, freqs) - delay_from_DM(dm0, freqs.max())
+    bins = np.round(d / dt).astype(int)
+    for c in range(C):
+        x[c, t0 + bins[c]:t0 + bins[c] + w] += 12
+    x = np.clip(x, 0, 255).astype(np.uint8)
+    dms = np.arange(0, 300, 2.0)
+    sw = DMSweep(dms, freqs, dt, dtype="u8")
+    plane = sw(torch.from_numpy(x).cuda(), trim=True)
+    cands = SinglePulseSearch(threshold=8.0)(plane, dms, dt)
+    best = cands[np.argmax(cands["Sigma"])]
+    assert abs(best["DM"] - dm0) <= 2.0 and abs(int(best["Sample"]) - t0) <= w
+    assert best["Sigma"] > 20

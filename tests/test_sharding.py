@@ -64,9 +64,25 @@ def _worker(rank, world, port, q):
         part = orc.sweep_plane(xb, tab, n_out=hi - lo)
         parts = [None] * world
         dist.all_gather_object(parts, part)
+        # DM-sharded sweep + local search: only candidates are exchanged
+        from oracle import search_oracle as so
+        from pypulsar_amd.search import to_records
+        xs = _data(C, N)
+        xs[:, 300:304] += 60.0  # undispersed burst: strongest near DM 0
+        xs = torch.from_numpy(xs) if rank == 0 else None
+
+        def search_fn(plane, sub):
+            c, _ = so.search(plane.numpy().astype(np.float64), (1, 2, 4, 8), 5.0, 200)
+            raw = np.array([(d, t, w, np.float32(s).view(np.int32)) for d, t, w, s in c],
+                           dtype=np.int32).reshape(-1, 4)
+            return to_records(raw, sub, DT)
+        cands = sharding.dm_sharded_search(xs, (C, N), torch.float32, dms, freqs, DT, n_out,
+                                           sweep_fn=_oracle_sweep(freqs, n_out),
+                                           search_fn=search_fn)
         if rank == 0:
             q.put(("dm", plane.numpy()))
             q.put(("tb", np.concatenate(parts, axis=1)))
+            q.put(("sp", cands))
     finally:
         dist.destroy_process_group()
 
@@ -80,7 +96,7 @@ def test_sharded_sweeps_equal_one_shot(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=240) for _ in range(2))
+    got = dict(q.get(timeout=240) for _ in range(3))
     for p in procs:
         p.join(timeout=240)
         assert p.exitcode == 0
@@ -91,6 +107,16 @@ def test_sharded_sweeps_equal_one_shot(world):
     want = orc.sweep_plane(_data(C, N).astype(np.float64), tab)
     np.testing.assert_array_equal(got["dm"].astype(np.float64), want)
     np.testing.assert_array_equal(got["tb"], want)
+    # sharded search == search of the one-shot plane
+    from oracle import search_oracle as so
+    xs = _data(C, N)
+    xs[:, 300:304] += 60.0
+    plane = orc.sweep_plane(xs.astype(np.float64), tab).astype(np.float32)
+    c, _ = so.search(plane.astype(np.float64), (1, 2, 4, 8), 5.0, 200)
+    sp = got["sp"]
+    assert len(sp) == len(c) > 0
+    want_k = sorted((dms[d], t, w) for d, t, w, s in c)
+    assert sorted(zip(sp["DM"], sp["Sample"], sp["Downfact"])) == want_k
 
 
 def test_dm_slices_balance():
