@@ -188,6 +188,19 @@ int pdd_sp_search(const float* x, int64_t D, int64_t n, int64_t ld, int64_t L, c
                   const float* istd, const int32_t* widths, int n_widths, float threshold,
                   int32_t* cands, int64_t max_cands, unsigned long long* count, void* stream);
 
+/* ---- PSRFITS search-mode subints -> [nchan][N] float32 (SURVEY.md §8(f)
+ * rank 3).  Replaces psrfits.unpack_4bit (formats/psrfits.py:37-50),
+ * PsrfitsFile.read_subint (:67-107: ((data*scales)+offsets)*weights in
+ * float32) and get_spectra (:140-183: concatenation, transpose, skip/trunc,
+ * band flip).  raw: nsub consecutive SUBINT table rows as stored (row_bytes
+ * each, big-endian; DATA at byte data_off of a row); nbits 4/8/16/32;
+ * wso: [nsub][3][nchan] float32 scales, offsets, weights; output row
+ * c' = flip ? nchan-1-c : c holds samples s0 .. s0+N-1 of the concatenated
+ * subints. */
+int pdd_psrfits_subints(const uint8_t* raw, int64_t nsub, int64_t row_bytes, int64_t data_off,
+                        int nbits, int64_t nsblk, int64_t nchan, const float* wso, int64_t s0,
+                        int64_t N, int flip, float* out, int64_t ld_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -28,7 +28,7 @@ EXPORTS = (
     "pdd_sweep_plan_destroy", "pdd_global_stats", "pdd_scale_rows", "pdd_masked_fill",
     "pdd_smooth", "pdd_zdm_downsample", "pdd_sweep_set_timing", "pdd_sweep_kernel_ms",
     "pdd_sweep_plan_create_grouped", "pdd_sweep_execute_grouped", "pdd_sp_chunk_stats",
-    "pdd_sp_search",
+    "pdd_sp_search", "pdd_psrfits_subints",
 )
 
 
@@ -72,6 +72,8 @@ _SIGS = {
     "pdd_sp_chunk_stats": ([_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp], _int),
     "pdd_sp_search": ([_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _int, ctypes.c_float, _vp,
                        _i64, _vp, _vp], _int),
+    "pdd_psrfits_subints": ([_vp, _i64, _i64, _i64, _int, _i64, _i64, _vp, _i64, _i64, _int, _vp,
+                             _i64, _vp], _int),
 }
 
 

@@ -1299,6 +1299,10 @@ __device__ __forceinline__ int stage_il_dma(uint32_t lds_dst, const float4* src,
 // compute waves publish done[b] -- measured slower: the sweep is bound by the
 // L2/MALL->LDS staging rate, ~80 CU-cycles per 1 KiB DMA, not by the barrier.)
 //
+// (Measured and dropped: the compute waves reading their shifts by scalar
+// loads from the global table instead -- SMEM shares lgkmcnt with the LDS
+// reads and returns out of order, so every counted LDS wait became
+// lgkmcnt(0): f32 43 -> 62 ms.)
 // Metadata: mt[dblk][c][ROW], ROW = DB + 4: the tile's DB shifts at channel c
 // relative to their minimum bmin, then {bmin, span, 0, 0}.  Every loader wave
 // DMAs the rows of chunk k into its own ring (slot k % MR) MA = NBUF chunks
@@ -1359,7 +1363,7 @@ __device__ __forceinline__ void il_tile_of(int bid, int n_tblk, int n_dblk, int 
 
 template <int G, int DPW, int NCW, int NLW, int CC, int NBUF, bool U16 = false>
 __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
-    const float4* __restrict__ R, int64_t nR, int C, int lo, const int* __restrict__ mt,
+    const float4* __restrict__ R0, int64_t nR, int C, int lo, const int* __restrict__ mt,
     float* __restrict__ out, int64_t ld_out, int D, int64_t Qs, int64_t t_base, int64_t n_out,
     int stride, int n_tblk, int n_dblk, int dbg, int64_t row_g, int64_t row_d) {
   // Grouped sweeps: C is the channel count of ONE group; blockIdx.x / (tiles
@@ -1379,18 +1383,26 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   const int buf_e = CC * stride;
   int* metar = reinterpret_cast<int*>(img + NBUF * buf_e);  // [NLW][MR][SLOT]
 
-  int dblk, tblk;
   const int per_grp = n_tblk * n_dblk;
-  const int grp = blockIdx.x / per_grp;
-  il_tile_of(blockIdx.x - grp * per_grp, n_tblk, n_dblk, dbg, dblk, tblk);
-  R += (int64_t)grp * C * nR;
-  const int64_t t0 = (int64_t)tblk * Tq;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int* mt_b = mt + ((int64_t)grp * n_dblk + dblk) * C * ROW;
   const int nchunk = (C + CC - 1) / CC;
   const bool stamps = (dbg & 4) != 0;  // dbg bit 2: per-wave cycle stamps into `out`
 
+  // One tile per workgroup.  (A persistent grid -- 256 workgroups walking
+  // their XCD's tiles in lockstep -- measured no faster: the L2 hit rate of
+  // the staging fell from 77% to 48% at unchanged kernel time, so the staging
+  // is not fabric-bound; and its loop-carried registers spilled.)
+#define IL_TILE_SETUP                                                         \
+  int dblk, tblk;                                                             \
+  const int grp = tile / per_grp;                                             \
+  il_tile_of(tile - grp * per_grp, n_tblk, n_dblk, dbg, dblk, tblk);          \
+  const float4* R = R0 + (int64_t)grp * C * nR;                               \
+  const int64_t t0 = (int64_t)tblk * Tq;                                      \
+  const int* mt_b = mt + ((int64_t)grp * n_dblk + dblk) * C * ROW;            \
+  (void)R; (void)t0; (void)mt_b;
+  const int tile = blockIdx.x;
+  IL_TILE_SETUP
   if (w >= NCW) {
     // ---------------- loader waves: metadata rows + sample windows
     // Top issue priority: a loader shares its SIMD with compute waves that
@@ -1472,13 +1484,16 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   // accumulated with plain 32-bit adds (two u16 lanes per add, no carry while
   // <= 257 channels of values <= 255 are summed) and flushed to float every
   // 256 channels -- exact.
-  float acc[DPW][G][S];
+  // accumulators as float pairs: the adds issue as v_pk_add_f32 (two samples
+  // per VALU instruction: half the issue slots of scalar v_add_f32)
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  f32x2_t acc[DPW][G][S / 2];
 #pragma unroll
   for (int j = 0; j < DPW; ++j)
 #pragma unroll
     for (int g = 0; g < G; ++g)
 #pragma unroll
-      for (int k2 = 0; k2 < S; ++k2) acc[j][g][k2] = 0.f;
+      for (int h = 0; h < S / 2; ++h) acc[j][g][h] = (f32x2_t){0.f, 0.f};
   uint32_t a16[U16 ? DPW : 1][U16 ? G : 1][4];
   if constexpr (U16) {
 #pragma unroll
@@ -1496,8 +1511,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
         for (int g = 0; g < G; ++g)
 #pragma unroll
           for (int h = 0; h < 4; ++h) {
-            acc[j][g][2 * h] += (float)(a16[j][g][h] & 0xffffu);
-            acc[j][g][2 * h + 1] += (float)(a16[j][g][h] >> 16);
+            acc[j][g][h] += (f32x2_t){(float)(a16[j][g][h] & 0xffffu), (float)(a16[j][g][h] >> 16)};
             a16[j][g][h] = 0u;
           }
     }
@@ -1530,8 +1544,8 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
         if (i >= ncc) break;
         const i32x4_t o =
             *(const lds_i32x4_t*)(uintptr_t)(meta_base + (uint32_t)((slot * SLOT + i * ROW) * 4));
-        const uint32_t cb = lane_byte + (uint32_t)((b * CC + i) * stride * 16);
         const int ov[4] = {o.x, o.y, o.z, o.w};
+        const uint32_t cb = lane_byte + (uint32_t)((b * CC + i) * stride * 16);
         if constexpr (U16) {
           // two trials at a time (a full scheduling barrier between the
           // halves keeps the live read registers within the 128-VGPR budget)
@@ -1570,18 +1584,19 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
           for (int j = 0; j < DPW; ++j)
 #pragma unroll
             for (int g2 = 0; g2 < G; ++g2) {
-              acc[j][g2][0] += v[j][g2].x;
-              acc[j][g2][1] += v[j][g2].y;
-              acc[j][g2][2] += v[j][g2].z;
-              acc[j][g2][3] += v[j][g2].w;
+              acc[j][g2][0] += v[j][g2].xy;
+              acc[j][g2][1] += v[j][g2].zw;
             }
-          __builtin_amdgcn_sched_group_barrier(0x100, 2 * G, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 4 * G, 0);
+          // one trial of reads in flight ahead of the adds (keeps the live read
+          // registers at 2 x 4G: the accumulators take 64 of the 128 VGPRs)
           __builtin_amdgcn_sched_group_barrier(0x100, G, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 4 * G, 0);
           __builtin_amdgcn_sched_group_barrier(0x100, G, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 4 * G, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 4 * G, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 2 * G, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, G, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 2 * G, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, G, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 2 * G, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 2 * G, 0);
         }
       }
     }
@@ -1606,10 +1621,11 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const int64_t t = t0 + g * 64 + lane;
-        if (t < Qs && t_base + t + k2 * Qs < n_out) orow[t + k2 * Qs] = acc[j][g][k2];
+        if (t < Qs && t_base + t + k2 * Qs < n_out) orow[t + k2 * Qs] = acc[j][g][k2 >> 1][k2 & 1];
       }
   }
 }
+#undef IL_TILE_SETUP
 
 // Host: pack each DM block's channel windows (16-element granules, the DMA
 // unit) into a ring of R elements in channel order; returns the largest
@@ -1684,7 +1700,13 @@ static const Variant kF32Variants[] = {{false, 4, 4, 4, 14, 2, 4, false, 0, 2, 1
                                        {false, 4, 4, 4, 8, 2, 3, true, 0},
                                        {false, 4, 4, 1, 8, 1, 2, false, 0},
                                        {false, 4, 1, 1, 1, 1, 2, false, 0}};
-static const Variant kU8Variants[] = {{false, 8, 2, 4, 14, 2, 4, false, 0, 2, 1},
+// u8: 12 compute + 4 loader waves first (32.5 vs 33.5 ms for 14 + 2 on
+// config 2: the u16 image halves the compute per staged byte, so the extra
+// loaders pay for themselves)
+static const Variant kU8Variants[] = {{false, 8, 2, 4, 12, 2, 4, false, 0, 4, 1},
+                                      {false, 8, 2, 4, 14, 2, 4, false, 0, 2, 1},
+                                      {false, 8, 2, 4, 14, 1, 8, false, 0, 2, 1},
+                                      {false, 8, 2, 4, 12, 1, 8, false, 0, 4, 1},
                                       {false, 4, 4, 4, 14, 2, 4, false, 0, 2, 1},
                                       {false, 4, 4, 4, 8, 1, 3, false, 0, 2, 1},
                                       {false, 4, 4, 4, 4, 1, 3, false, 0, 2, 1},
@@ -1707,8 +1729,15 @@ static sweep_il_fn il_kernel_for(const Variant& v) {
   if (v.S == 4 && v.NW == NCW_ && v.ws == NLW_ && v.CC == CC_ && v.NBUF == NB_ && v.G == 4 &&  \
       v.DPW == 4)                                                                              \
     return k_sweep_il<4, 4, NCW_, NLW_, CC_, NB_>;
-  if (v.S == 8 && v.NW == 14 && v.ws == 2 && v.CC == 2 && v.NBUF == 4 && v.G == 2 && v.DPW == 4)
-    return k_sweep_il<2, 4, 14, 2, 2, 4, true>;
+#define IL16(NCW_, NLW_, CC_, NB_)                                                           \
+  if (v.S == 8 && v.NW == NCW_ && v.ws == NLW_ && v.CC == CC_ && v.NBUF == NB_ && v.G == 2 &&  \
+      v.DPW == 4)                                                                              \
+    return k_sweep_il<2, 4, NCW_, NLW_, CC_, NB_, true>;
+  IL16(14, 2, 2, 4)
+  IL16(14, 2, 1, 8)
+  IL16(12, 4, 2, 4)
+  IL16(12, 4, 1, 8)
+#undef IL16
   IL(14, 2, 1, 8)
   IL(14, 2, 2, 4)
   IL(8, 2, 1, 6)
@@ -1864,7 +1893,7 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
               "pdd_sweep_plan_create: bad extents D=%lld C=%lld", (long long)D, (long long)C);
   PDD_REQUIRE(dtype == PDD_F32 || dtype == PDD_U8, "pdd_sweep_plan_create: dtype must be F32 or U8");
   const Variant* cands = dtype == PDD_U8 ? kU8Variants : kF32Variants;
-  const int ncand = dtype == PDD_U8 ? 8 : 15;
+  const int ncand = dtype == PDD_U8 ? 11 : 15;
 
   const int fv = forced_variant();
   for (int vi = (fv >= 0 && fv < ncand) ? fv : 0; vi < ncand; ++vi) {
