@@ -8,8 +8,8 @@ trim=True) -> downsample -> scaled -> smooth -> plot, with every step a HIP
 kernel and only the final 2-D image and summed series copied to the host.
 
 Differences from the reference, all where it cannot run:
-  * ``--mask`` needs PRESTO's rfifind (absent) and ``.fits`` input needs the
-    PSRFITS reader (out of scope): both raise a clear error;
+  * ``--mask`` needs PRESTO's rfifind (absent): it raises a clear error;
+    ``.fits`` input goes through pypulsar_amd.formats.psrfits (device decode);
   * with dm == 0 the reference's ``dmtime`` is unbound (waterfaller.py:193-196):
     here it is 0;
   * ``-n/--nbins`` is honoured when no duration is given (the reference
@@ -33,7 +33,8 @@ def open_data_file(fn):
     if fn.endswith(".fil"):
         return filterbank.filterbank(fn)
     if fn.endswith(".fits"):
-        raise ValueError("PSRFITS input is not supported by this build (filterbank only)")
+        from pypulsar_amd.formats import psrfits
+        return psrfits.PsrfitsFile(fn)
     raise ValueError("Cannot recognize data file type from extension. "
                      "(Only '.fits' and '.fil' are supported.)")
 

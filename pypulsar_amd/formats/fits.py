@@ -221,23 +221,25 @@ def write(fn, primary_cards, tables):
     """Write a primary HDU (no data) + BINTABLE extensions.
 
     ``tables``: list of (extname, header cards, columns, rows) where columns
-    is [(name, tform)] and rows a structured array whose fields are the
-    column names (any endianness; written big-endian)."""
+    is [(name, tform)] and rows maps each column name to its per-row values
+    (a dict of arrays or a structured array; any endianness, written
+    big-endian)."""
     with builtins.open(fn, "wb") as f:
         cards = [("SIMPLE", True), ("BITPIX", 8), ("NAXIS", 0), ("EXTEND", True)]
         f.write(_header_bytes(cards + list(primary_cards)))
         for extname, hcards, columns, rows in tables:
+            nrows = len(rows[columns[0][0]]) if columns else 0
             cols = [Column(n, t, 0) for n, t in columns]
             width = sum(c.nbytes for c in cols)
             cards = [("XTENSION", "BINTABLE"), ("BITPIX", 8), ("NAXIS", 2), ("NAXIS1", width),
-                     ("NAXIS2", len(rows)), ("PCOUNT", 0), ("GCOUNT", 1),
+                     ("NAXIS2", nrows), ("PCOUNT", 0), ("GCOUNT", 1),
                      ("TFIELDS", len(cols))]
             for i, (n, t) in enumerate(columns):
                 cards += [("TTYPE%d" % (i + 1), n), ("TFORM%d" % (i + 1), t)]
             cards += [("EXTNAME", extname)] + list(hcards)
             f.write(_header_bytes(cards))
             dt = np.dtype([c.np_field() for c in cols])
-            out = np.zeros(len(rows), dtype=dt)
+            out = np.zeros(nrows, dtype=dt)
             for c in cols:
                 out[c.name] = rows[c.name]
             b = out.tobytes()

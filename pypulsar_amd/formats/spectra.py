@@ -135,6 +135,22 @@ class Spectra(object):
         self.starttime = starttime
         self.dm = 0  # the reference ignores the dm argument (spectra.py:37)
 
+    @classmethod
+    def _from_device(cls, freqs, dt, x, starttime=0):
+        """Adopt a float32 [numchans, numspectra] device tensor produced by a
+        reader kernel (no copy; the readers' own data, so the reference's
+        always-copy constructor semantics are kept)."""
+        assert x.dtype == torch.float32 and x.dim() == 2 and x.stride(1) == 1
+        self = cls.__new__(cls)
+        self.numchans, self.numspectra = x.shape
+        assert len(freqs) == self.numchans
+        self.freqs = freqs
+        self._x, self._raw8 = x, None
+        self.dt = dt
+        self.starttime = starttime
+        self.dm = 0
+        return self
+
     # ------------------------------------------------------------ data access
     @property
     def device_data(self):

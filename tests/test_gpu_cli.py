@@ -96,3 +96,28 @@ def test_waterfaller_cli(gpu, tmp_path):
     d = orc.smooth(orc.scaled(d), 3, "mean")
     assert data.data.shape == d.shape
     assert rel_err(data.data, d) <= 1e-5
+
+
+def test_waterfaller_psrfits(gpu, tmp_path):
+    """waterfaller.py on a PSRFITS file (waterfaller.py:58-59 opens .fits with
+    psrfits.PsrfitsFile): same pipeline result as on a filterbank holding the
+    same spectra (scales 1, offsets 0, weights 1; descending band)."""
+    from pypulsar_amd.bin import waterfaller as w
+    from pypulsar_amd.formats.psrfits import write_search_psrfits
+    C, nsblk, nsub = 64, 1000, 12
+    x = u8_data(C, nsblk * nsub, 21)                     # [C, N]
+    fil = _fil(tmp_path, x.T.copy())
+    from pypulsar_amd.formats import filterbank as fbm
+    freqs = fbm.filterbank(fil).freqs                    # descending, as written
+    fits_fn = str(tmp_path / "wf.fits")
+    write_search_psrfits(fits_fn, x.T.reshape(nsub, nsblk, C), freqs, DT, 8)
+    png = str(tmp_path / "wf2.png")
+    assert w.main(["-T", "0.01", "-n", "2000", "-d", "100", "-s", "16", "--outfile", png,
+                   fits_fn]) == 0
+    assert os.path.getsize(png) > 1000
+    opts = type("O", (), dict(dm=100.0, start=0.01, duration=None, nbins=2000, maskfile=None,
+                              width_bins=1, downsamp=1, nsub=16, subdm=100.0, scaleindep=False))
+    a = w.run(fits_fn, opts).data
+    b = w.run(fil, opts).data
+    assert a.shape == b.shape
+    np.testing.assert_array_equal(a, b)
