@@ -33,11 +33,11 @@ def per_kernel(pattern, counter):
 
 def main():
     os.makedirs(DST, exist_ok=True)
-    for name in ("f32", "u8", "stream", "subband"):
+    for name in ("f32", "u8", "stream", "subband", "search"):
         f = glob.glob(os.path.join(SRC, "kt_" + name, "**", "*kernel_stats.csv"), recursive=True)
         if f:
             shutil.copy(f[0], os.path.join(DST, "%s_%s_kernel_stats.csv" % (TAG, name)))
-    for name in ("f32", "u8", "stream", "subband"):
+    for name in ("f32", "u8", "stream", "subband", "search"):
         f = os.path.join(SRC, "bench_%s.json" % name)
         if os.path.exists(f):
             lines = [l for l in open(f) if l.startswith("{")]

@@ -15,6 +15,8 @@ python -c "import __graft_entry__ as g; g.build()" > $O/build.log 2>&1 \
  && timeout -k 10 300 python bench.py --config stream --steps 6 --warmup 2 > $O/bench_stream.json 2> $O/bench_stream.err && echo BENCH_STREAM_OK \
  && timeout -k 10 300 python bench.py --config subband --steps 3 --warmup 1 > $O/bench_subband.json 2> $O/bench_subband.err && echo BENCH_SUBBAND_OK \
  && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_stream -o kt --output-format csv -- python bench.py --config stream --steps 4 --warmup 1 > $O/kt_stream.log 2>&1 \
+ && timeout -k 10 300 python bench.py --config search --steps 5 --warmup 2 > $O/bench_search.json 2> $O/bench_search.err && echo BENCH_SEARCH_OK \
+ && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_search -o kt --output-format csv -- python bench.py --config search --steps 5 --warmup 2 > $O/kt_search.log 2>&1 \
  && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_subband -o kt --output-format csv -- python bench.py --config subband --steps 3 --warmup 1 --no-cpu-baseline > $O/kt_subband.log 2>&1 \
  && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_f32 -o kt --output-format csv -- python bench.py $BA > $O/kt_f32.log 2>&1 \
  && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_u8 -o kt --output-format csv -- python bench.py $BA --dtype u8 > $O/kt_u8.log 2>&1 \
