@@ -183,10 +183,18 @@ int pdd_sp_chunk_stats(const float* x, int64_t D, int64_t n, int64_t ld, int64_t
  * int32 records {row, start, width, float-bits snr} through the device
  * counter *count (incremented for every candidate, stored while
  * < max_cands: the caller checks for overflow).  Record order is not
- * deterministic; the set is. */
+ * deterministic; the set is.
+ * Streams: a row may continue into a second plane -- row d is
+ * x[d][0:n] followed by x_next[d][0:n_next] (n % L == 0; its chunks use
+ * mean_next/istd_next, [D][ceil(n_next/L)]) -- and only starts < n_starts
+ * are searched, so block i of a stream is searched with the first columns
+ * of block i+1 exactly as the one-shot plane would be.  n_next = 0 (and
+ * null next pointers): a single plane. */
 int pdd_sp_search(const float* x, int64_t D, int64_t n, int64_t ld, int64_t L, const float* mean,
-                  const float* istd, const int32_t* widths, int n_widths, float threshold,
-                  int32_t* cands, int64_t max_cands, unsigned long long* count, void* stream);
+                  const float* istd, const float* x_next, int64_t n_next, int64_t ld_next,
+                  const float* mean_next, const float* istd_next, int64_t n_starts,
+                  const int32_t* widths, int n_widths, float threshold, int32_t* cands,
+                  int64_t max_cands, unsigned long long* count, void* stream);
 
 /* ---- PSRFITS search-mode subints -> [nchan][N] float32 (SURVEY.md §8(f)
  * rank 3).  Replaces psrfits.unpack_4bit (formats/psrfits.py:37-50),

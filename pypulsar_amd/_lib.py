@@ -70,8 +70,8 @@ _SIGS = {
                                    _vp], _int),
     "pdd_sweep_kernel_ms": ([_vp, ctypes.POINTER(ctypes.c_float)], _int),
     "pdd_sp_chunk_stats": ([_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp], _int),
-    "pdd_sp_search": ([_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _int, ctypes.c_float, _vp,
-                       _i64, _vp, _vp], _int),
+    "pdd_sp_search": ([_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i64,
+                       _vp, _int, ctypes.c_float, _vp, _i64, _vp, _vp], _int),
     "pdd_psrfits_subints": ([_vp, _i64, _i64, _i64, _int, _i64, _i64, _vp, _i64, _i64, _int, _vp,
                              _i64, _vp], _int),
 }

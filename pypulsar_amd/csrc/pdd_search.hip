@@ -25,6 +25,7 @@
 //                (start, width) is one LDS difference; per-window max, then
 //                an exact arg-max pass only for windows over the threshold;
 //                compact candidate list through one atomic counter.
+#include <algorithm>
 #include <cmath>
 
 #include "pdd_internal.h"
@@ -105,8 +106,10 @@ __global__ __launch_bounds__(256) void k_sp_stats(const float* __restrict__ x, i
 //           first (width, start) in (width, start) order whose S/N -- the
 //           same float ops, hence bit-identical -- equals that maximum.
 __global__ __launch_bounds__(kSpThreads) void k_sp_search(
-    const float* __restrict__ x, int64_t n, int64_t ld, int64_t L, int64_t nchunk,
-    const float* __restrict__ mean, const float* __restrict__ istd, Widths W, float thr,
+    const float* __restrict__ x, int64_t na, int64_t ld, const float* __restrict__ xn,
+    int64_t ldn, int64_t n, int64_t n_starts, int64_t L, int64_t nchunk, int64_t nchunk_n,
+    const float* __restrict__ mean, const float* __restrict__ istd,
+    const float* __restrict__ mean_n, const float* __restrict__ istd_n, Widths W, float thr,
     int64_t nblk, int32_t* __restrict__ cands, int64_t max_cands,
     unsigned long long* __restrict__ count) {
   __shared__ float P[kSpSpan + 1];
@@ -117,11 +120,17 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_search(
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t d = blockIdx.x / nblk, blk = blockIdx.x % nblk;
   const int64_t t0 = blk * kSpStarts;
+  // the row is x[d][0:na] followed by xn[d][0:n-na] (a stream's next plane);
+  // chunks k < nchunk use mean/istd, later ones mean_n/istd_n (na % L == 0)
   const float* row = x + d * ld;
+  const float* nrow = xn ? xn + d * ldn - na : row;
   const float* mrow = mean + d * nchunk;
   const float* irow = istd + d * nchunk;
+  const float* mnrow = mean_n ? mean_n + d * nchunk_n - nchunk : mrow;
+  const float* inrow = istd_n ? istd_n + d * nchunk_n - nchunk : irow;
   const int64_t span = min((int64_t)kSpStarts + W.maxw - 1, n - t0);  // z values needed
   const int64_t nst = n - t0;  // start i is valid for width w when i + w <= nst
+  const int64_t nss = n_starts - t0;  // ... and i < nss
 
   // z of the starts + halo, coalesced, into P[1..]; the chunk index advances
   // incrementally (one 64-bit division per thread, not per sample)
@@ -135,7 +144,9 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_search(
           ++k;
           nb += L;
         }
-        z = (__builtin_nontemporal_load(row + t) - mrow[k]) * irow[k];
+        const bool a = t < na;
+        const float v = __builtin_nontemporal_load((a ? row : nrow) + t);
+        z = (v - (k < nchunk ? mrow : mnrow)[k]) * (k < nchunk ? irow : inrow)[k];
       }
       P[i + 1] = z;
     }
@@ -174,7 +185,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_search(
   float m[kSpWpb];
 #pragma unroll
   for (int q = 0; q < kSpWpb; ++q) m[q] = -INFINITY;
-  if (nst >= kSpStarts - 1 + W.maxw) {
+  if (nst >= kSpStarts - 1 + W.maxw && nss >= kSpStarts) {
     // interior block: every (start, width) valid; starts in pairs through
     // packed f32 (v_pk_add_f32 / v_pk_mul_f32), maxima through v_max3_f32
     for (int wi = 0; wi < W.n; ++wi) {
@@ -197,7 +208,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_search(
 #pragma unroll
       for (int r = 0; r < kSpR; ++r) {
         const int i = tid + kSpThreads * r;
-        const float snr = (i + w <= nst) ? (P[i + w] - p0[r]) * iw : -INFINITY;
+        const float snr = (i + w <= nst && i < nss) ? (P[i + w] - p0[r]) * iw : -INFINITY;
         m[r / (kSpR / kSpWpb)] = fmaxf(m[r / (kSpR / kSpWpb)], snr);
       }
     }
@@ -231,7 +242,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_search(
 #pragma unroll
     for (int r = 0; r < kSpR; ++r) {
       const int i = tid + kSpThreads * r, q = r / (kSpR / kSpWpb);
-      const float snr = (i + w <= nst) ? (P[i + w] - p0[r]) * iw : -INFINITY;
+      const float snr = (i + w <= nst && i < nss) ? (P[i + w] - p0[r]) * iw : -INFINITY;
       if (bmax[q] >= thr && snr == bmax[q]) key[q] = min(key[q], wi * kSpStarts + i);
     }
   }
@@ -279,11 +290,17 @@ int pdd_sp_chunk_stats(const float* x, int64_t D, int64_t n, int64_t ld, int64_t
 }
 
 int pdd_sp_search(const float* x, int64_t D, int64_t n, int64_t ld, int64_t L, const float* mean,
-                  const float* istd, const int32_t* widths, int n_widths, float threshold,
-                  int32_t* cands, int64_t max_cands, unsigned long long* count, void* stream) {
+                  const float* istd, const float* x_next, int64_t n_next, int64_t ld_next,
+                  const float* mean_next, const float* istd_next, int64_t n_starts,
+                  const int32_t* widths, int n_widths, float threshold, int32_t* cands,
+                  int64_t max_cands, unsigned long long* count, void* stream) {
   PDD_REQUIRE(x && mean && istd && widths && count && (cands || max_cands == 0),
               "pdd_sp_search: null pointer");
   PDD_REQUIRE(D >= 0 && n > 0 && ld >= n && L > 0 && max_cands >= 0, "pdd_sp_search: bad shape");
+  PDD_REQUIRE(n_next >= 0 && (n_next == 0 || (x_next && mean_next && istd_next &&
+                                               ld_next >= n_next && n % L == 0)),
+              "pdd_sp_search: next plane needs x/mean/istd, ld >= n_next and n %% L == 0");
+  PDD_REQUIRE(n_starts >= 0 && n_starts <= n + n_next, "pdd_sp_search: n_starts out of range");
   PDD_REQUIRE(n_widths >= 1 && n_widths <= kSpMaxWidths, "pdd_sp_search: 1..%d widths",
               kSpMaxWidths);
   Widths W;
@@ -297,12 +314,15 @@ int pdd_sp_search(const float* x, int64_t D, int64_t n, int64_t ld, int64_t L, c
     W.inv_sqrt[i] = (float)(1.0 / std::sqrt((double)widths[i]));
     W.maxw = widths[i];
   }
-  const int64_t nchunk = cdiv(n, L);
-  const int64_t nblk = cdiv(n, kSpStarts);
-  PDD_REQUIRE(D * nblk < (1ll << 31) && n < (1ll << 31) - kSpSpan, "pdd_sp_search: too large");
-  if (D == 0) return 0;
+  const int64_t nchunk = cdiv(n, L), nchunk_n = cdiv(n_next, L);
+  const int64_t nt = n + n_next;
+  const int64_t nblk = cdiv(std::min(n_starts, nt), kSpStarts);
+  PDD_REQUIRE(D * nblk < (1ll << 31) && nt < (1ll << 31) - kSpSpan, "pdd_sp_search: too large");
+  if (D == 0 || nblk == 0) return 0;
   k_sp_search<<<(unsigned)(D * nblk), kSpThreads, 0, as_stream(stream)>>>(
-      x, n, ld, L, nchunk, mean, istd, W, threshold, nblk, cands, max_cands, count);
+      x, n, ld, n_next ? x_next : nullptr, ld_next, nt, n_starts, L, nchunk, nchunk_n, mean, istd,
+      n_next ? mean_next : nullptr, n_next ? istd_next : nullptr, W, threshold, nblk, cands,
+      max_cands, count);
   PDD_LAUNCHED();
   return 0;
 }

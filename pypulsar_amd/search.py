@@ -57,38 +57,108 @@ class SinglePulseSearch(object):
         assert self.detrendlen >= 1
         self.max_cands = int(max_cands)
 
-    def raw(self, plane, stream=None):
-        """Device-side search; returns (cands int32 [k, 4] = row, start, width,
-        snr bits, count tensor) without synchronising."""
+    def stats(self, plane, stream=None):
+        """Per-chunk (mean, 1/std) of a [D, n] plane: [D, ceil(n/L)] each."""
         assert plane.is_cuda and plane.dtype == torch.float32 and plane.dim() == 2
         assert plane.stride(1) == 1
         D, n = plane.shape
-        dev = plane.device
         nchunk = -(-n // self.detrendlen)
-        mean = torch.empty((D, nchunk), dtype=torch.float32, device=dev)
+        mean = torch.empty((D, nchunk), dtype=torch.float32, device=plane.device)
         istd = torch.empty_like(mean)
+        if D and n:
+            call("pdd_sp_chunk_stats", ptr(plane), D, n, plane.stride(0), self.detrendlen,
+                 ptr(mean), ptr(istd), stream_ptr(stream))
+        return mean, istd
+
+    def raw(self, plane, stream=None, stats=None, nxt=None, n_starts=None):
+        """Device-side search; returns (cands int32 [max_cands, 4] = row,
+        start, width, snr bits; count tensor) without synchronising.
+        ``nxt`` = (next plane, its stats): the rows continue into the next
+        plane of a stream (plane width must be a multiple of detrendlen);
+        ``n_starts`` limits the searched starts (default: all)."""
+        D, n = plane.shape
+        dev = plane.device
+        mean, istd = self.stats(plane, stream) if stats is None else stats
         cands = torch.empty((self.max_cands, 4), dtype=torch.int32, device=dev)
         count = torch.zeros(1, dtype=torch.int64, device=dev)
         if D == 0 or n == 0:
             return cands[:0], count
-        s = stream_ptr(stream)
-        call("pdd_sp_chunk_stats", ptr(plane), D, n, plane.stride(0), self.detrendlen, ptr(mean),
-             ptr(istd), s)
+        xn, n_next, ldn, mn, sn = None, 0, 0, None, None
+        if nxt is not None:
+            xn, (mn, sn) = nxt
+            assert xn.shape[0] == D and xn.stride(1) == 1
+            assert n % self.detrendlen == 0, "a continued plane needs width % detrendlen == 0"
+            n_next, ldn = xn.shape[1], xn.stride(0)
+            nc = -(-n_next // self.detrendlen)  # the next plane's chunks in use
+            mn, sn = mn[:, :nc].contiguous(), sn[:, :nc].contiguous()
+        if n_starts is None:
+            n_starts = n + n_next
         call("pdd_sp_search", ptr(plane), D, n, plane.stride(0), self.detrendlen, ptr(mean),
-             ptr(istd), self.widths.ctypes.data_as(ctypes.c_void_p), len(self.widths),
-             ctypes.c_float(self.threshold), ptr(cands), self.max_cands, ptr(count), s)
+             ptr(istd), ptr(xn) if n_next else None, n_next, ldn,
+             ptr(mn) if n_next else None, ptr(sn) if n_next else None, n_starts,
+             self.widths.ctypes.data_as(ctypes.c_void_p), len(self.widths),
+             ctypes.c_float(self.threshold), ptr(cands), self.max_cands, ptr(count),
+             stream_ptr(stream))
         return cands, count
+
+    def collect(self, cands, count, dms, dt, t0=0, starttime=0.0):
+        """Device (cands, count) -> sorted candidate records (synchronises)."""
+        k = int(count.item())
+        if k > self.max_cands:
+            raise RuntimeError("single-pulse search: %d candidates exceed max_cands=%d "
+                               "(raise the threshold or max_cands)" % (k, self.max_cands))
+        return to_records(cands[:k].cpu().numpy(), dms, dt, t0, starttime)
 
     def __call__(self, plane, dms, dt, t0=0, starttime=0.0, stream=None):
         dms = np.atleast_1d(np.asarray(dms, dtype=np.float64))
         assert len(dms) == plane.shape[0], "one DM per plane row"
         cands, count = self.raw(plane, stream)
-        k = int(count.item())
-        if k > self.max_cands:
-            raise RuntimeError("single-pulse search: %d candidates exceed max_cands=%d "
-                               "(raise the threshold or max_cands)" % (k, self.max_cands))
-        c = cands[:k].cpu().numpy()
-        return to_records(c, dms, dt, t0, starttime)
+        return self.collect(cands, count, dms, dt, t0, starttime)
+
+
+class StreamingSearch(object):
+    """Streaming FRB pipeline: ``StreamingSweep`` blocks (zero-DM, downsample,
+    DM sweep; BASELINE config 5) searched one block behind the sweep, each
+    block's rows continued into the next block's plane, so the candidates
+    equal those of a one-shot search of the whole stream's plane.  Needs the
+    plane block width (block / downsamp) to be a multiple of the detrend
+    length and of the 1024-start window.  Yields candidate record arrays.
+    Preallocated ``planes`` (see StreamingSweep) must number at least 2: a
+    block's plane is read again when the next block's plane is searched."""
+
+    def __init__(self, dms, freqs, dt, block=1 << 18, downsamp=2, zero_dm=True, dtype=None,
+                 threshold=6.0, widths=DEFAULT_WIDTHS, detrendlen=1024, max_cands=1 << 20):
+        from .stream import StreamingSweep
+        kw = {} if dtype is None else {"dtype": dtype}
+        self.sweep = StreamingSweep(dms, freqs, dt, block=block, downsamp=downsamp,
+                                    zero_dm=zero_dm, **kw)
+        self.search = SinglePulseSearch(threshold, widths, detrendlen, max_cands)
+        nb = self.sweep.n_out_block
+        assert nb % detrendlen == 0 and nb % WINDOW == 0, \
+            "block/downsamp must be a multiple of detrendlen and of %d" % WINDOW
+        self.dms = np.asarray(dms, dtype=np.float64)
+        self.dt = dt * downsamp
+
+    def __call__(self, chunks, planes=None, starttime=0.0):
+        assert planes is None or len(planes) >= 2
+        halo = int(self.search.widths[-1]) - 1
+        prev = None  # (t0, plane, stats)
+        for t0, plane in self.sweep(chunks, planes):
+            st = self.search.stats(plane)
+            if prev is not None:
+                p0, pp, ps = prev
+                h = min(halo, plane.shape[1])
+                c, k = self.search.raw(pp, stats=ps, nxt=(plane[:, :h], st) if h else None,
+                                       n_starts=pp.shape[1])
+                yield self.search.collect(c, k, self.dms, self.dt, p0, starttime)
+            prev = (t0, plane, st)
+        if prev is not None:
+            p0, pp, ps = prev
+            c, k = self.search.raw(pp, stats=ps)
+            yield self.search.collect(c, k, self.dms, self.dt, p0, starttime)
+
+    def close(self):
+        self.sweep.close()
 
 
 def to_records(c, dms, dt, t0=0, starttime=0.0):

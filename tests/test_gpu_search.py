@@ -11,6 +11,7 @@ from oracle import search_oracle as so
 
 pytestmark = pytest.mark.gpu
 WIDTHS = (1, 2, 3, 4, 6, 9, 14, 20, 30, 45, 70, 100, 150)
+DT = 64e-6
 
 
 def _check(gpu_c, ora, margins, thr):
@@ -97,3 +98,48 @@ def test_sweep_then_search_finds_dispersed_pulse(gpu):
     best = cands[np.argmax(cands["Sigma"])]
     assert abs(best["DM"] - dm0) <= 2.0 and abs(int(best["Sample"]) - t0) <= w
     assert best["Sigma"] > 20
+
+
+@pytest.mark.parametrize("nchunks,last", [(4, 8192), (3, 3000)])
+def test_streaming_search_equals_one_shot(gpu, nchunks, last):
+    """StreamingSearch (blocks searched one behind the sweep, rows continued
+    into the next block's plane) finds exactly the candidates of a one-shot
+    search of the whole stream's plane, including pulses straddling block
+    boundaries."""
+    import torch
+    from pypulsar_amd import _lib
+    from pypulsar_amd._lib import call, ptr, stream_ptr
+    from pypulsar_amd.search import SinglePulseSearch, StreamingSearch
+    from pypulsar_amd.sweep import DMSweep
+    C, block, ds = 64, 8192, 2
+    freqs = band(C)
+    dms = np.linspace(0.0, 60.0, 24)
+    N = block * (nchunks - 1) + last
+    rng = np.random.default_rng(3)
+    x = np.clip(np.round(rng.normal(128, 16, (N, C))), 0, 255).astype(np.uint8)
+    # bursts dispersed at DM 30 (zero-DM would remove undispersed ones), the
+    # first two arriving (at the top of the band) just before block seams
+    from pypulsar_amd.delays import delay_from_DM
+    bins = np.round((delay_from_DM(30.0, freqs) - delay_from_DM(30.0, freqs.max())) / DT)
+    xi = x.astype(np.int32)
+    for t in (block - 20, 2 * block - 3, block + 1000):
+        for c in range(C):
+            b = t + int(bins[c])
+            xi[b:b + 12, c] += 40
+    x = np.clip(xi, 0, 255).astype(np.uint8)
+    widths = (1, 2, 4, 8, 16, 32)
+    ss = StreamingSearch(dms, freqs, DT, block=block, downsamp=ds, threshold=5.0, widths=widths,
+                         detrendlen=1024)
+    chunks = [torch.from_numpy(x[i:i + block]).pin_memory() for i in range(0, N, block)]
+    got = np.concatenate(list(ss(chunks)))
+    ss.close()
+    xd = torch.from_numpy(x).cuda()
+    f32 = torch.empty((C, N // ds), dtype=torch.float32, device="cuda")
+    call("pdd_zdm_downsample", ptr(xd), _lib.U8, N, C, C, ds, 1, ptr(f32), f32.stride(0),
+         stream_ptr())
+    plane = DMSweep(dms, freqs, DT * ds)(f32)
+    want = SinglePulseSearch(threshold=5.0, widths=widths, detrendlen=1024)(plane, dms, DT * ds)
+    assert len(want) > 0
+    key = lambda r: sorted(zip(r["row"], r["Sample"], r["Downfact"]))
+    assert key(got) == key(want)
+    np.testing.assert_array_equal(np.sort(got["Sigma"]), np.sort(want["Sigma"]))
