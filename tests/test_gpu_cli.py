@@ -121,3 +121,29 @@ def test_waterfaller_psrfits(gpu, tmp_path):
     b = w.run(fil, opts).data
     assert a.shape == b.shape
     np.testing.assert_array_equal(a, b)
+
+
+def test_frb_search_cli(gpu, tmp_path):
+    """frb_search.py end to end: a burst dispersed at DM 40 in a 3-block
+    8-bit filterbank comes out of the .singlepulse file at its DM and time."""
+    from pypulsar_amd.bin import frb_search as fs
+    from pypulsar_amd.delays import delay_from_DM
+    from pypulsar_amd.search import read_singlepulse
+    C, N, block = 128, 3 * 8192, 8192
+    x = u8_data(C, N, 31).astype(np.int32).T.copy()     # [N, C] file order
+    fn0 = _fil(tmp_path, x.astype(np.uint8))
+    from pypulsar_amd.formats import filterbank as fbm
+    freqs = fbm.filterbank(fn0).freqs
+    bins = np.round((delay_from_DM(40.0, freqs) - delay_from_DM(40.0, freqs.max())) / DT)
+    t_arr = 9000
+    for c in range(C):
+        x[t_arr + int(bins[c]):t_arr + int(bins[c]) + 8, c] += 30
+    fn = _fil(tmp_path, np.clip(x, 0, 255).astype(np.uint8), name="burst.fil")
+    out = str(tmp_path / "burst.singlepulse")
+    assert fs.main(["--lodm", "0", "--hidm", "80", "--numdms", "81", "--downsamp", "2",
+                    "--block", str(block), "-t", "8", "-o", out, fn]) == 0
+    cands = read_singlepulse(out)
+    assert len(cands) >= 1
+    best = cands[np.argmax(cands["Sigma"])]
+    assert abs(best["DM"] - 40.0) <= 2.0
+    assert abs(best["Time"] - t_arr * DT) <= 16 * DT
