@@ -182,6 +182,8 @@ def main():
     ap.add_argument("--mode", default="timeblock", choices=["timeblock", "dmshard"])
     ap.add_argument("--cpu-trials", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--search", action="store_true",
+                    help="stream: also boxcar-search every block (StreamingSearch)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -393,7 +395,13 @@ def stream_bench(args, cfg, rank, world, dev):
     dt = 64e-6
     freqs = band(C)
     dms = np.linspace(cfg["dm_lo"], cfg["dm_hi"], D)
-    st = StreamingSweep(dms, freqs, dt, block=block, downsamp=ds)
+    if args.search:
+        from pypulsar_amd.search import StreamingSearch
+        ss = StreamingSearch(dms, freqs, dt, block=block, downsamp=ds, threshold=8.0,
+                             detrendlen=1024)
+        st = ss.sweep
+    else:
+        st = StreamingSweep(dms, freqs, dt, block=block, downsamp=ds)
     # two distinct pinned chunks, reused cyclically (content is irrelevant to speed)
     chunks = []
     for i in range(2):
@@ -406,10 +414,16 @@ def stream_bench(args, cfg, rank, world, dev):
     nb = st.n_out_block
     planes = [torch.empty((D, nb), dtype=torch.float32, device=dev) for _ in range(3)]
     total = args.warmup + args.steps + 1  # +1: a block is emitted when the next chunk arrives
-    gen = st((chunks[i % 2] for i in range(total)), planes=planes)
+    if args.search:  # searched one block behind the sweep
+        gen = ss((chunks[i % 2] for i in range(total + 1)), planes=planes)
+    else:
+        gen = st((chunks[i % 2] for i in range(total)), planes=planes)
     done = 0
     t0 = None
-    for _, plane in gen:
+    ncand = 0
+    for item in gen:
+        if args.search:
+            ncand += len(item)
         done += 1
         if done == args.warmup:
             torch.cuda.synchronize()
@@ -437,8 +451,10 @@ def stream_bench(args, cfg, rank, world, dev):
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic uint8 clip(round(N(128,16))) blocks in pinned host memory",
         "config": {"workload": "streaming: %d-ch u8 blocks of %d spectra (pinned H2D, async) + "
-                               "zero-DM (float) + downsample %d + %d-DM sweep (0-%g pc/cc)"
-                               % (C, block, ds, D, cfg["dm_hi"]),
+                               "zero-DM (float) + downsample %d + %d-DM sweep (0-%g pc/cc)%s"
+                               % (C, block, ds, D, cfg["dm_hi"],
+                                  " + boxcar search (13 widths, S/N 8)" if args.search else ""),
+                   "candidates": ncand if args.search else None,
                    "config_name": "stream", "channels": C, "block": block, "overlap": st.ov,
                    "downsamp": ds, "dm_trials": D, "parallelism": "tb%d" % world},
         "realtime_factor": (block * dt) / (ms * 1e-3),
