@@ -10,8 +10,10 @@ per step per rank / time.
 
 Multi-GPU (torchrun, one rank per GPU): time-block sharding -- every rank
 sweeps its OWN block (seeded by rank) over the full DM grid, no data-path
-collective ("scaling": "weak"); --mode dmshard instead broadcasts ONE block
-over RCCL and gives each rank a DM slice (pypulsar_amd.sharding).
+collective ("scaling": "weak"); --mode dmshard instead shards ONE block's DM
+grid ("strong"): each step all-gathers the block from the ranks' 1/N slices
+over RCCL, corner-turns it and sweeps the rank's DM slice
+(pypulsar_amd.sharding; planes stay resident for a downstream search).
 
 Timing: W untimed warm-up steps, then exactly K steps bracketed by a barrier
 + torch.cuda.synchronize(); the max over ranks is reported.  The sweep
@@ -218,10 +220,18 @@ def main():
         dms = dms_all
         x = synth_block(C, N, 1000 + rank, args.dtype, dev)
     else:
-        from pypulsar_amd.sharding import dm_slices
+        # DM sharding (strong scaling): each rank holds 1/world of the
+        # time-major block; every step all-gathers it over RCCL, corner-turns
+        # it on the device and sweeps this rank's DM slice (sharding.py)
+        from pypulsar_amd import _lib
+        from pypulsar_amd._lib import call, ptr, stream_ptr
+        from pypulsar_amd.sharding import allgather_block, dm_slices
         lo, hi = dm_slices(D, world)[rank]
         dms = dms_all[lo:hi]
-        x = synth_block(C, N, 1000, args.dtype, dev)
+        assert N % world == 0
+        part = synth_block(N // world, C, 1000 + rank, args.dtype, dev)  # [N/world, C]
+        x = torch.empty((C, N), dtype=part.dtype, device=dev)
+        code = _lib.U8 if args.dtype == "u8" else _lib.F32
     sw = DMSweep(dms, freqs, dt, dtype=args.dtype)
     # plane width of the full grid (trim=True): identical on every rank
     full_max = int(DMSweep(dms_all[-1:], freqs, dt).max_bin)
@@ -229,6 +239,9 @@ def main():
     plane = torch.empty((len(dms), n_out), dtype=torch.float32, device=dev)
 
     def step():
+        if args.mode != "timeblock":
+            blk = allgather_block(part) if world > 1 else part
+            call("pdd_corner_turn", ptr(blk), code, N, C, C, ptr(x), code, N, stream_ptr())
         return sw(x, out=plane)
 
     for _ in range(args.warmup):

@@ -79,7 +79,19 @@ def _worker(rank, world, port, q):
         cands = sharding.dm_sharded_search(xs, (C, N), torch.float32, dms, freqs, DT, n_out,
                                            sweep_fn=_oracle_sweep(freqs, n_out),
                                            search_fn=search_fn)
+        # all-gather exchange: each rank holds 1/world of the time-major block
+        xt = _data(C, N).T.copy()  # [N, C]
+        nr = -(-N // world)
+        xt = np.concatenate([xt, np.zeros((nr * world - N, C), np.float32)])
+        part = torch.from_numpy(xt[rank * nr:(rank + 1) * nr].copy())
+        (lo, hi), mine = sharding.dm_sharded_sweep_ag(
+            part, dms, freqs, DT, n_out, sweep_fn=_oracle_sweep(freqs, n_out),
+            to_cm=lambda b: b[:N].t().contiguous())
+        ag = [None] * world
+        dist.all_gather_object(ag, (lo, hi, None if mine is None else mine.numpy()))
         if rank == 0:
+            q.put(("ag", np.concatenate([p for _, _, p in sorted(ag, key=lambda a: a[0])
+                                         if p is not None])))
             q.put(("dm", plane.numpy()))
             q.put(("tb", np.concatenate(parts, axis=1)))
             q.put(("sp", cands))
@@ -96,7 +108,7 @@ def test_sharded_sweeps_equal_one_shot(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=240) for _ in range(3))
+    got = dict(q.get(timeout=240) for _ in range(4))
     for p in procs:
         p.join(timeout=240)
         assert p.exitcode == 0
@@ -107,6 +119,7 @@ def test_sharded_sweeps_equal_one_shot(world):
     want = orc.sweep_plane(_data(C, N).astype(np.float64), tab)
     np.testing.assert_array_equal(got["dm"].astype(np.float64), want)
     np.testing.assert_array_equal(got["tb"], want)
+    np.testing.assert_array_equal(got["ag"].astype(np.float64), want)
     # sharded search == search of the one-shot plane
     from oracle import search_oracle as so
     xs = _data(C, N)
