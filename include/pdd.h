@@ -88,6 +88,11 @@ int pdd_shift_group_sum(const float* x, int64_t C, int64_t N, int64_t ld, const 
  * Replaces Spectra.downsample (formats/spectra.py:329-351). */
 int pdd_downsample(const float* x, int64_t C, int64_t N, int64_t ld, int64_t factor,
                    float* out, int64_t ld_out, void* stream);
+/* The same on 8-bit channel rows (a Spectra's unmodified raw bytes): exact
+ * integer sums, written as float32; reads a quarter of the float32 image's
+ * bytes.  Used by the DDplan executor (spectra.py:329-351 per DDstep). */
+int pdd_downsample_u8(const uint8_t* x, int64_t C, int64_t N, int64_t ld, int64_t factor,
+                      float* out, int64_t ld_out, void* stream);
 
 /* Zero-DM filter: every spectrum minus its channel mean; integer data use
  * round-half-even of the float64 mean and wrap modulo 2^nbits, float32 data

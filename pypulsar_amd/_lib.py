@@ -28,7 +28,7 @@ EXPORTS = (
     "pdd_sweep_plan_destroy", "pdd_global_stats", "pdd_scale_rows", "pdd_masked_fill",
     "pdd_smooth", "pdd_zdm_downsample", "pdd_sweep_set_timing", "pdd_sweep_kernel_ms",
     "pdd_sweep_plan_create_grouped", "pdd_sweep_execute_grouped", "pdd_sp_chunk_stats",
-    "pdd_sp_search", "pdd_psrfits_subints",
+    "pdd_sp_search", "pdd_psrfits_subints", "pdd_downsample_u8",
 )
 
 
@@ -54,6 +54,7 @@ _SIGS = {
     "pdd_shift_group_sum": ([_vp, _i64, _i64, _i64, _vp, _int, _vp, _i64, _vp, _i64, _i64, _vp],
                             _int),
     "pdd_downsample": ([_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp], _int),
+    "pdd_downsample_u8": ([_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp], _int),
     "pdd_zero_dm": ([_vp, _int, _i64, _i64, _i64, _int, _vp, _i64, _vp], _int),
     "pdd_sweep_plan_create": ([_vp, _i64, _i64, _int, ctypes.POINTER(_vp)], _int),
     "pdd_sweep_execute": ([_vp, _vp, _i64, _i64, _int, _vp, _vp, _i64, _i64, _vp], _int),

@@ -221,6 +221,43 @@ __global__ __launch_bounds__(256) void k_downsample(const float* __restrict__ x,
   out[c * ld_out + j] = (float)s;
 }
 
+// 8-bit input (a Spectra's raw bytes): integer sums (exact), one 16-byte load
+// per lane when the factor divides 16 and the rows are 16-B aligned -- a
+// quarter of the float32 image's bytes (DDplan executor, spectra.py:329-351)
+__global__ __launch_bounds__(256) void k_downsample_u8v(const uint8_t* __restrict__ x, int64_t ld,
+                                                        int factor, int64_t nvec,
+                                                        float* __restrict__ out, int64_t ld_out,
+                                                        int64_t nout, int64_t tiles) {
+  const int64_t c = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const int64_t v = tile * 256 + threadIdx.x;  // 16-byte vector index in the row
+  if (v >= nvec) return;
+  const uint4 q = *reinterpret_cast<const uint4*>(x + c * ld + v * 16);
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+  const int per = 16 / factor;  // outputs per vector
+  float* o = out + c * ld_out + v * per;
+  for (int k = 0; k < per; ++k) {
+    uint32_t s = 0;
+    for (int b = 0; b < factor; ++b) {
+      const int e = k * factor + b;
+      s += (w[e >> 2] >> (8 * (e & 3))) & 0xffu;
+    }
+    if (v * per + k < nout) o[k] = (float)s;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_downsample_u8(const uint8_t* __restrict__ x, int64_t ld,
+                                                       int64_t factor, int64_t nout,
+                                                       float* __restrict__ out, int64_t ld_out,
+                                                       int64_t tiles) {
+  const int64_t c = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const int64_t j = tile * 256 + threadIdx.x;
+  if (j >= nout) return;
+  const uint8_t* p = x + c * ld + j * factor;
+  uint64_t s = 0;
+  for (int64_t k = 0; k < factor; ++k) s += p[k];
+  out[c * ld_out + j] = (float)s;
+}
+
 // ---------------------------------------------------------------- zero-DM
 // Integer data: avg = rint(float64(sum)/nchan) cast to the dtype, out = x - avg
 // modulo 2^nbits (bin/zero_dm_filter.py:35-39).  float32: float32 mean.
@@ -675,6 +712,31 @@ int pdd_downsample(const float* x, int64_t C, int64_t N, int64_t ld, int64_t fac
   PDD_REQUIRE(C * tiles < (1ll << 31), "pdd_downsample: too large");
   k_downsample<<<(unsigned)(C * tiles), 256, 0, as_stream(stream)>>>(x, ld, factor, nout, out,
                                                                      ld_out, tiles);
+  PDD_LAUNCHED();
+  return 0;
+}
+
+int pdd_downsample_u8(const uint8_t* x, int64_t C, int64_t N, int64_t ld, int64_t factor,
+                      float* out, int64_t ld_out, void* stream) {
+  PDD_REQUIRE(x && out, "pdd_downsample_u8: null pointer");
+  PDD_REQUIRE(factor >= 1 && C >= 0 && N >= 0 && ld >= N, "pdd_downsample_u8: bad shape");
+  const int64_t nout = N / factor;
+  PDD_REQUIRE(ld_out >= nout, "pdd_downsample_u8: ld_out too small");
+  if (C == 0 || nout == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  const bool vec = (16 % factor == 0) && ((uintptr_t)x % 16 == 0) && (ld % 16 == 0);
+  if (vec) {
+    const int64_t nvec = cdiv(nout * factor, 16);  // the last vector may read past nout*factor
+    PDD_REQUIRE(nvec * 16 <= ld, "pdd_downsample_u8: row padding");
+    const int64_t tiles = cdiv(nvec, 256);
+    PDD_REQUIRE(C * tiles < (1ll << 31), "pdd_downsample_u8: too large");
+    k_downsample_u8v<<<(unsigned)(C * tiles), 256, 0, s>>>(x, ld, (int)factor, nvec, out, ld_out,
+                                                          nout, tiles);
+  } else {
+    const int64_t tiles = cdiv(nout, 256);
+    PDD_REQUIRE(C * tiles < (1ll << 31), "pdd_downsample_u8: too large");
+    k_downsample_u8<<<(unsigned)(C * tiles), 256, 0, s>>>(x, ld, factor, nout, out, ld_out, tiles);
+  }
   PDD_LAUNCHED();
   return 0;
 }

@@ -227,6 +227,11 @@ def execute_plan_grouped(spectra, ddplan, padval=0):
     from .formats.spectra import _pad_args
     results = []
     src = spectra.device_data
+    # the raw 8-bit rows when the Spectra still holds them unmodified: the
+    # downsample then reads a quarter of the bytes (exact integer sums)
+    raw8 = getattr(spectra, "_raw8", None)
+    if raw8 is not None and (tuple(raw8.shape) != tuple(src.shape) or raw8.stride(1) != 1):
+        raw8 = None
     for step in ddplan.DDsteps:
         # downsampled view of the data (Spectra.downsample semantics, without
         # copying or modifying the caller's Spectra)
@@ -235,7 +240,10 @@ def execute_plan_grouped(spectra, ddplan, padval=0):
             C0, N0 = src.shape
             n_ds = N0 // step.downsamp
             x = torch.empty((C0, n_ds), dtype=torch.float32, device=src.device)
-            if n_ds:
+            if n_ds and raw8 is not None:
+                call("pdd_downsample_u8", ptr(raw8), C0, N0, raw8.stride(0), step.downsamp, ptr(x),
+                     n_ds, stream_ptr())
+            elif n_ds:
                 call("pdd_downsample", ptr(src), C0, N0, src.stride(0), step.downsamp, ptr(x), n_ds,
                      stream_ptr())
         else:

@@ -76,3 +76,24 @@ def test_grouped_two_stage_golden(gpu, golden, golden_meta):
     out = torch.empty(want.shape, device="cuda")
     g2(sub, want.shape[1], out, row_g=0, row_d=1)
     np.testing.assert_array_equal(out.cpu().numpy().astype(np.float64), want)
+
+
+@pytest.mark.parametrize("factor", [1, 2, 3, 4, 8, 16, 32])
+@pytest.mark.parametrize("N", [4096, 4099])
+def test_downsample_u8_equals_f32(gpu, factor, N):
+    """pdd_downsample_u8 (the DDplan executor's path for unmodified 8-bit
+    Spectra) == pdd_downsample on the float image == the oracle, bit-exact."""
+    import torch
+    from pypulsar_amd._lib import call, ptr, stream_ptr
+    C = 37
+    x = u8_data(C, N, factor)
+    xu = torch.from_numpy(x).cuda()
+    xf = xu.float()
+    n = N // factor
+    a = torch.zeros((C, n), device="cuda")
+    b = torch.zeros((C, n), device="cuda")
+    call("pdd_downsample_u8", ptr(xu), C, N, N, factor, ptr(a), n, stream_ptr())
+    call("pdd_downsample", ptr(xf), C, N, N, factor, ptr(b), n, stream_ptr())
+    want, _ = orc.downsample(x.astype(np.float64), DT, factor)
+    np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
+    np.testing.assert_array_equal(a.cpu().numpy().astype(np.float64), want)
