@@ -184,6 +184,9 @@ def main():
     ap.add_argument("--mode", default="timeblock", choices=["timeblock", "dmshard"])
     ap.add_argument("--cpu-trials", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e", action="store_true",
+                    help="also time one PCIe-inclusive step: pinned host block -> H2D -> "
+                         "sweep -> D2H of the plane into pinned host memory")
     ap.add_argument("--search", action="store_true",
                     help="stream: also boxcar-search every block (StreamingSearch)")
     args = ap.parse_args()
@@ -267,6 +270,26 @@ def main():
         ks.append(sw.kernel_ms())
     sw.set_timing(False)
     kern_ms = float(np.mean(ks))
+    e2e = None
+    if args.e2e and args.mode == "timeblock":
+        # PCIe-inclusive: the boundary handed host buffers
+        hx = torch.empty(x.shape, dtype=x.dtype, pin_memory=True)
+        hx.copy_(x)
+        hp = torch.empty(plane.shape, dtype=plane.dtype, pin_memory=True)
+        xd = torch.empty_like(x)
+        ms = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            xd.copy_(hx, non_blocking=True)
+            sw(xd, out=plane)
+            hp.copy_(plane, non_blocking=True)
+            torch.cuda.synchronize()
+            ms.append((time.perf_counter() - t1) * 1e3)
+        e2e = {"ms_per_step": min(ms), "value": len(dms) * n_out * C / (min(ms) * 1e-3),
+               "bytes_h2d": x.numel() * x.element_size(), "bytes_d2h": plane.numel() * 4,
+               "note": "best of 3; value = samples*channels*DM/s including the transfers"}
+        del hx, hp, xd
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -324,6 +347,8 @@ def main():
                              "bytes_per_launch": uniq_bytes},
             "cpu_baseline": None,
         }
+        if e2e is not None:
+            line["end_to_end_pcie"] = e2e
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_trials, dt)
         print(json.dumps(line))
