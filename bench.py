@@ -50,6 +50,9 @@ CONFIGS = {
     "subband": dict(C=4096, N=1 << 20, nsub=64, dm_lo=0.0, dm_hi=1000.0, res=0.5),
     # single-pulse search over the config2 plane
     "search": dict(C=1024, N=1 << 20, D=1024, dm_lo=0.0, dm_hi=1000.0),
+    # HBM-bound single-DM kernels at a large block,
+    # plus BASELINE.json configs[0] (waterfaller dedisperse, 1024 x 2^16, DM 100)
+    "ops": dict(C=4096, N=1 << 18, wf_C=1024, wf_N=1 << 16, wf_dm=100.0),
 }
 
 
@@ -214,6 +217,8 @@ def main():
         return subband_bench(args, cfg, rank, world, dev)
     if args.config == "search":
         return search_bench(args, cfg, rank, world, dev)
+    if args.config == "ops":
+        return ops_bench(args, cfg, rank, world, dev)
     C, N, D = cfg["C"], cfg["N"], cfg["D"]
     dt = 64e-6
     freqs = band(C)
@@ -363,6 +368,131 @@ def _finish(args, world, line):
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def ops_bench(args, cfg, rank, world, dev):
+    """HBM roofline of the single-DM kernels (read the input
+    once + write the output once = the algorithmic bytes) on a C x N block
+    resident in HBM, each timed with HIP events on the stream it runs on
+    (torch's current stream), mean of --steps launches after --warmup; and
+    BASELINE.json configs[0] -- Spectra.dedisperse(100, padval, trim=True) +
+    channel sum of a 1024 x 2^16 8-bit filterbank -- through the drop-in
+    Spectra API (device-resident data), with the NumPy oracle of the same
+    call on one host core beside it.  Rank-local: every rank measures its own
+    GPU (no collective in this mode); rank 0 prints."""
+    from pypulsar_amd import _lib
+    from pypulsar_amd._lib import call, ptr, stream_ptr
+    from pypulsar_amd.formats.spectra import Spectra
+    C, N = cfg["C"], cfg["N"]
+    x8t = synth_block(N, C, 7 + rank, "u8", dev)           # [N, C] filterbank order
+    x8 = x8t.t().contiguous()                              # [C, N] raw bytes
+    xf = x8.float()                                        # [C, N] float32
+    freqs = band(C)
+    from pypulsar_amd.delays import dedisperse_bins
+    bins = torch.from_numpy(np.asarray(dedisperse_bins(1000.0, freqs, 64e-6), dtype=np.int32)).to(dev)
+    zero = torch.zeros(C, dtype=torch.float32, device=dev)
+    o_cn = torch.empty((C, N), dtype=torch.float32, device=dev)
+    o_ds = torch.empty((C, N // 4), dtype=torch.float32, device=dev)
+    o_zt = torch.empty((N, C), dtype=torch.uint8, device=dev)
+    o_sub = torch.empty((64, N), dtype=torch.float32, device=dev)
+    o_ser = torch.empty((1, N), dtype=torch.float32, device=dev)
+    o_c = torch.empty(C, dtype=torch.float32, device=dev)
+    o_zd = torch.empty((C, N // 2), dtype=torch.float32, device=dev)
+    st = stream_ptr()
+    F, U8 = _lib.F32, _lib.U8
+    cn4, cn1 = C * N * 4, C * N
+    ops = [
+        ("shift_pad (dedisperse, pad 0)", "Spectra.shift_channels spectra.py:54-94", cn4 + cn4,
+         lambda: call("pdd_shift_pad", ptr(xf), C, N, N, ptr(bins), _lib.PAD_VALUE, ptr(zero),
+                      ptr(o_cn), N, N, st)),
+        ("shift_group_sum nsub=1 (dedispersed series)", "dedisperse + waterfaller.py:140",
+         cn4 + N * 4,
+         lambda: call("pdd_shift_group_sum", ptr(xf), C, N, N, ptr(bins), _lib.PAD_VALUE,
+                      ptr(zero), 1, ptr(o_ser), N, N, st)),
+        ("shift_group_sum nsub=64 (subband)", "Spectra.subband spectra.py:96-138",
+         cn4 + 64 * N * 4,
+         lambda: call("pdd_shift_group_sum", ptr(xf), C, N, N, ptr(bins), _lib.PAD_VALUE,
+                      ptr(zero), 64, ptr(o_sub), N, N, st)),
+        ("downsample f32 x4", "Spectra.downsample spectra.py:329-351", cn4 + cn4 // 4,
+         lambda: call("pdd_downsample", ptr(xf), C, N, N, 4, ptr(o_ds), N // 4, st)),
+        ("downsample u8 x4", "Spectra.downsample (raw 8-bit rows)", cn1 + cn4 // 4,
+         lambda: call("pdd_downsample_u8", ptr(x8), C, N, N, 4, ptr(o_ds), N // 4, st)),
+        ("zero_dm u8 time-major (wrap)", "zero_dm_filter.py:30-50", cn1 + cn1,
+         lambda: call("pdd_zero_dm", ptr(x8t), U8, N, C, C, _lib.LAYOUT_TIME_MAJOR, ptr(o_zt),
+                      C, st)),
+        ("corner_turn u8 [N,C] -> f32 [C,N]", "filterbank.get_spectra .T + astype",
+         cn1 + cn4,
+         lambda: call("pdd_corner_turn", ptr(x8t), U8, N, C, C, ptr(o_cn), F, N, st)),
+        ("zdm_downsample u8 x2 (stream prologue)", "zero-DM + downsample + corner turn",
+         cn1 + cn4 // 2,
+         lambda: call("pdd_zdm_downsample", ptr(x8t), U8, N, C, C, 2, 1, ptr(o_zd), N // 2,
+                      st)),
+        ("channel_stats mean", "shift_channels padval='mean' spectra.py:83-86", cn4 + C * 4,
+         lambda: call("pdd_channel_stats", ptr(xf), C, N, N, _lib.STAT_MEAN, ptr(o_c), st)),
+        ("smooth width 8", "Spectra.smooth spectra.py:262-303", cn4 + cn4,
+         lambda: call("pdd_smooth", ptr(xf), C, N, N, 8, _lib.PAD_VALUE, ptr(zero), ptr(o_cn),
+                      N, st)),
+    ]
+    rows = []
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for name, ref, nbytes, fn in ops:
+        for _ in range(max(1, args.warmup)):
+            fn()
+        torch.cuda.synchronize()
+        ev0.record()
+        for _ in range(args.steps):
+            fn()
+        ev1.record()
+        torch.cuda.synchronize()
+        ms = ev0.elapsed_time(ev1) / args.steps
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        rows.append({"kernel": name, "reference": ref, "bytes": nbytes, "ms": ms,
+                     "achieved_GBs": gbs, "frac_hbm": gbs / PEAK_HBM_GBS})
+
+    # BASELINE.json configs[0] through the drop-in API
+    wC, wN, wdm = cfg["wf_C"], cfg["wf_N"], cfg["wf_dm"]
+    wfreqs = band(wC)
+    w8 = synth_block(wC, wN, 11, "u8", dev)
+    wf = {}
+    for pad in (0, "mean"):
+        def one():
+            s = Spectra(wfreqs, 64e-6, w8)  # the reference constructor: u8 -> float copy
+            s.dedisperse(wdm, padval=pad, trim=True)
+            return s.sum_channels()
+        for _ in range(3):
+            one()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            ser = one()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / args.steps * 1e3
+        wf["padval_%s" % pad] = {"ms": ms, "n_out": int(ser.shape[-1])}
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        from oracle import spectra_oracle as orc
+        xh = w8.cpu().numpy().astype(np.float64)
+        cpu = {}
+        for pad in (0, "mean"):
+            t0 = time.perf_counter()
+            out, _ = orc.dedisperse(xh, wfreqs, 64e-6, wdm, padval=pad, trim=True)
+            out.sum(axis=0)
+            cpu["padval_%s" % pad] = {"ms": (time.perf_counter() - t0) * 1e3}
+        cpu.update({"cores": 1, "kind": "port", "cpu_model": _cpu_model(),
+                    "sample": "the same call on the same block (float64 NumPy, C-order, 1 thread)"})
+    if rank == 0:
+        line = {"metric": "HBM roofline of the single-DM kernels (algorithmic bytes / kernel time)",
+                "value": float(np.mean([r["frac_hbm"] for r in rows])),
+                "unit": "mean fraction of 8 TB/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "higher_is_better": True, "dtype": "f32/u8",
+                "data": "synthetic (uint8 clip(round(N(128,16))), generated on device)",
+                "config": {"workload": "single-DM ops on %d ch x 2^%d samples (DM 1000 shifts, "
+                                       "1250-1550 MHz, 64 us); configs[0] waterfaller "
+                                       "dedisperse %d ch x 2^%d at DM %g"
+                                       % (C, int(np.log2(N)), wC, int(np.log2(wN)), wdm),
+                           "config_name": "ops"},
+                "ops": rows, "waterfaller_config0": {"gpu": wf, "cpu_baseline": cpu}}
+        print(json.dumps(line))
 
 
 def search_bench(args, cfg, rank, world, dev):

@@ -4,6 +4,7 @@
 // bounded by HBM (≈8 TB/s spec).  Algorithmic bytes per launch are documented
 // in DESIGN.md §Kernels.  Coalescing: consecutive lanes always touch
 // consecutive samples of one channel row (wave-strided, 64 lanes x 4 B).
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstring>
@@ -50,6 +51,41 @@ __global__ __launch_bounds__(256) void k_corner_turn(const InT* __restrict__ in,
   }
 }
 
+// The same to float32 with 16-byte row loads (8 lanes cover one 128-byte
+// line of a spectrum): tile = 64 spectra x 8*VEC channels, VEC = elements per
+// 16 bytes.  Rows must be 16-B aligned and nchan*sizeof(InT) a multiple of 16
+// (the launcher checks).
+template <typename InT>
+__global__ __launch_bounds__(256) void k_corner_turn_vec(const InT* __restrict__ in, int64_t nspec,
+                                                         int64_t nchan, int64_t ld_in,
+                                                         float* __restrict__ out, int64_t ld_out,
+                                                         int64_t tiles_c) {
+  constexpr int VEC = 16 / sizeof(InT);
+  constexpr int TC = 8 * VEC;
+  __shared__ float tile[TC][65];
+  const int64_t tt = blockIdx.x / tiles_c, tc = blockIdx.x % tiles_c;
+  const int64_t t0 = tt * 64, c0 = tc * TC;
+  const int seg = threadIdx.x & 7, r0 = threadIdx.x >> 3;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int i = r0 + 32 * pass;
+    const int64_t t = t0 + i, c = c0 + seg * VEC;
+    union { uint4 q; InT e[VEC]; } u;
+    if (t < nspec && c < nchan) u.q = *reinterpret_cast<const uint4*>(in + t * ld_in + c);
+    else u.q = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) tile[seg * VEC + e][i] = static_cast<float>(u.e[e]);
+  }
+  __syncthreads();
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t t = t0 + tx;
+#pragma unroll 4
+  for (int i = ty; i < TC; i += 4) {
+    const int64_t c = c0 + i;
+    if (t < nspec && c < nchan) out[c * ld_out + t] = tile[i][tx];
+  }
+}
+
 template <typename InT>
 __global__ __launch_bounds__(256) void k_convert(const InT* __restrict__ in, int64_t rows,
                                                  int64_t cols, int64_t ld_in,
@@ -73,13 +109,32 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
   return v;
 }
 
-// Per-channel mean in float64 (one workgroup per channel).
+// Per-channel mean in float64 (one workgroup per channel); 16-byte loads,
+// four in flight per lane, when the rows are 16-B aligned.
 __global__ __launch_bounds__(256) void k_channel_mean(const float* __restrict__ x, int64_t N,
                                                       int64_t ld, float* __restrict__ out) {
   __shared__ double part[4];
   const float* row = x + (int64_t)blockIdx.x * ld;
   double s = 0.0;
-  for (int64_t i = threadIdx.x; i < N; i += 256) s += (double)row[i];
+  int64_t i0 = 0;
+  if (((uintptr_t)row & 15) == 0) {
+    const float4* r4 = reinterpret_cast<const float4*>(row);
+    const int64_t n4 = N / 4;
+    int64_t i = threadIdx.x;
+    for (; i + 768 < n4; i += 1024) {
+      float4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = r4[i + 256 * k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += ((double)v[k].x + (double)v[k].y) + ((double)v[k].z + (double)v[k].w);
+    }
+    for (; i < n4; i += 256) {
+      const float4 v = r4[i];
+      s += ((double)v.x + (double)v.y) + ((double)v.z + (double)v.w);
+    }
+    i0 = n4 * 4;
+  }
+  for (int64_t i = i0 + threadIdx.x; i < N; i += 256) s += (double)row[i];
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
   __syncthreads();
@@ -174,37 +229,77 @@ __global__ __launch_bounds__(256) void k_shift_pad(const float* __restrict__ x, 
 
 // ---------------------------------------------------------------- shift + group sum
 // out[g][t] = sum_{c in group g} X(c, t + bins[c]).  Block = 256 outputs of
-// one group; wave w sums channels c = w, w+4, ... of the group in float64,
-// then the 4 partials are added in a fixed order (deterministic).
-__global__ __launch_bounds__(256) void k_shift_group_sum(
+// one group (4 per lane) and one of `csplit` channel slices of it; wave w of
+// 8 sums channels w, w+8, ... of the slice in float64, four channels' loads
+// in flight at once (16 per lane: enough bytes in flight to reach HBM rate);
+// the 8 partials are added in a fixed order (deterministic).  csplit > 1
+// (few outputs per group) writes float64 partials that k_group_sum_reduce
+// adds in slice order.
+constexpr int kGsWaves = 8;
+__global__ __launch_bounds__(kGsWaves * 64) void k_shift_group_sum(
     const float* __restrict__ x, int64_t N, int64_t ld, const int32_t* __restrict__ bins,
-    int pad_mode, const float* __restrict__ padvals, int64_t cps, float* __restrict__ out,
-    int64_t ld_out, int64_t n_out, int64_t tiles) {
-  __shared__ double part[4][256];
-  const int64_t g = blockIdx.x / tiles, tile = blockIdx.x % tiles;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int pad_mode, const float* __restrict__ padvals, int64_t cps, int64_t csplit,
+    float* __restrict__ out, double* __restrict__ part_out, int64_t ld_out, int64_t n_out,
+    int64_t tiles, int64_t ngrp) {
+  __shared__ double part[kGsWaves][256];
+  const int64_t gp = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const int64_t g = gp % ngrp, sl = gp / ngrp;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int64_t cpp = (cps + csplit - 1) / csplit;
+  const int64_t cbeg = sl * cpp, cend = min(cps, cbeg + cpp);
   const int64_t t0 = tile * 256 + lane;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int64_t ci = w; ci < cps; ci += 4) {
-    const int64_t c = g * cps + ci;
-    const float* row = x + c * ld;
-    int64_t b = bins ? (int64_t)bins[c] : 0;
-    if (pad_mode == PDD_PAD_ROTATE) b = ((b % N) + N) % N;
-    const float pad = (pad_mode == PDD_PAD_VALUE && padvals) ? padvals[c] : 0.f;
+  for (int64_t ci = cbeg + w; ci < cend; ci += 4 * kGsWaves) {
+    float v[4][4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t t = t0 + 64 * k;
-      if (t < n_out) acc[k] += (double)fetch_padded(row, t + b, N, pad_mode, pad);
+    for (int j = 0; j < 4; ++j) {
+      const int64_t cj = ci + j * kGsWaves;
+      if (cj < cend) {
+        const int64_t c = g * cps + cj;
+        const float* row = x + c * ld;
+        int64_t b = bins ? (int64_t)bins[c] : 0;
+        if (pad_mode == PDD_PAD_ROTATE) b = ((b % N) + N) % N;
+        const float pad = (pad_mode == PDD_PAD_VALUE && padvals) ? padvals[c] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t t = t0 + 64 * k;
+          v[j][k] = (t < n_out) ? fetch_padded(row, t + b, N, pad_mode, pad) : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[j][k] = 0.f;
+      }
     }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] += (double)v[j][k];
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k) part[w][lane + 64 * k] = acc[k];
   __syncthreads();
-  const int64_t t = tile * 256 + threadIdx.x;
-  if (t < n_out) {
+  if (threadIdx.x < 256) {
     const int i = threadIdx.x;
-    out[g * ld_out + t] = (float)((part[0][i] + part[1][i]) + (part[2][i] + part[3][i]));
+    const int64_t t = tile * 256 + i;
+    if (t < n_out) {
+      const double sum = ((part[0][i] + part[1][i]) + (part[2][i] + part[3][i])) +
+                         ((part[4][i] + part[5][i]) + (part[6][i] + part[7][i]));
+      if (csplit == 1) out[g * ld_out + t] = (float)sum;
+      else part_out[(sl * ngrp + g) * n_out + t] = sum;
+    }
   }
+}
+
+__global__ __launch_bounds__(256) void k_group_sum_reduce(const double* __restrict__ part,
+                                                          int64_t csplit, int64_t ngrp,
+                                                          int64_t n_out, float* __restrict__ out,
+                                                          int64_t ld_out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= ngrp * n_out) return;
+  const int64_t g = i / n_out, t = i % n_out;
+  double s = 0.0;
+  for (int64_t p = 0; p < csplit; ++p) s += part[(p * ngrp + g) * n_out + t];
+  out[g * ld_out + t] = (float)s;
 }
 
 // ---------------------------------------------------------------- downsample
@@ -218,6 +313,26 @@ __global__ __launch_bounds__(256) void k_downsample(const float* __restrict__ x,
   const float* p = x + c * ld + j * factor;
   double s = 0.0;
   for (int64_t k = 0; k < factor; ++k) s += (double)p[k];
+  out[c * ld_out + j] = (float)s;
+}
+
+// factor % 4 == 0 and 16-B aligned rows: float4 loads (factor/4 per output)
+__global__ __launch_bounds__(256) void k_downsample_v4(const float* __restrict__ x, int64_t ld,
+                                                       int64_t factor, int64_t nout,
+                                                       float* __restrict__ out, int64_t ld_out,
+                                                       int64_t tiles) {
+  const int64_t c = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const int64_t j = tile * 256 + threadIdx.x;
+  if (j >= nout) return;
+  const float4* p = reinterpret_cast<const float4*>(x + c * ld + j * factor);
+  double s = 0.0;
+  for (int64_t k = 0; k < factor / 4; ++k) {
+    const float4 v = p[k];
+    s += (double)v.x;
+    s += (double)v.y;
+    s += (double)v.z;
+    s += (double)v.w;
+  }
   out[c * ld_out + j] = (float)s;
 }
 
@@ -296,6 +411,52 @@ __global__ __launch_bounds__(256) void k_zero_dm_tm(const T* __restrict__ in, in
   }
   T* orow = out + s * ld_out;
   for (int64_t c = lane; c < nchan; c += 64) orow[c] = zd_apply<T>(row[c], mean);
+}
+
+// 8/16-bit time-major rows, 16 bytes per lane per load (rows 16-B aligned,
+// nchan*sizeof(T) a multiple of 16; the launcher checks): one wave per
+// spectrum, the byte/halfword sum by masked SWAR adds, and the modular
+// subtraction of the rounded mean applied to whole words without borrows
+// between lanes: ((x | H) - (a & ~H)) ^ ((x ^ ~a) & H), H = the lane sign bits.
+template <typename T>
+__global__ __launch_bounds__(256) void k_zero_dm_tm_vec(const T* __restrict__ in, int64_t nspec,
+                                                        int64_t nchan, int64_t ld,
+                                                        T* __restrict__ out, int64_t ld_out) {
+  static_assert(sizeof(T) == 1 || sizeof(T) == 2, "8/16-bit only");
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (s >= nspec) return;
+  const uint4* row = reinterpret_cast<const uint4*>(in + s * ld);
+  const int64_t nv = nchan * (int64_t)sizeof(T) / 16;
+  constexpr uint32_t M = sizeof(T) == 1 ? 0x00ff00ffu : 0x0000ffffu;
+  constexpr int SH = sizeof(T) == 1 ? 8 : 16;
+  unsigned long long acc = 0;
+  for (int64_t v = lane; v < nv; v += 64) {
+    const uint4 q = row[v];
+    const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+    uint32_t p = 0;  // two 16-bit (u8) / one 32-bit-safe (u16: split below) partial lanes
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (sizeof(T) == 1) p += (w4[i] & M) + ((w4[i] >> SH) & M);
+      else acc += (unsigned long long)((w4[i] & M) + (w4[i] >> SH));
+    }
+    if constexpr (sizeof(T) == 1) acc += (unsigned long long)((p & 0xffffu) + (p >> 16));
+  }
+  acc = wave_sum_u64(acc);
+  acc = __shfl(acc, 0, 64);
+  const uint32_t a = (uint32_t)rint((double)acc / (double)nchan);
+  constexpr uint32_t H = sizeof(T) == 1 ? 0x80808080u : 0x80008000u;
+  const uint32_t ar = sizeof(T) == 1 ? (a & 0xffu) * 0x01010101u : (a & 0xffffu) * 0x00010001u;
+  uint4* orow = reinterpret_cast<uint4*>(out + s * ld_out);
+  for (int64_t v = lane; v < nv; v += 64) {
+    const uint4 q = row[v];
+    uint4 r;
+    r.x = ((q.x | H) - (ar & ~H)) ^ ((q.x ^ ~ar) & H);
+    r.y = ((q.y | H) - (ar & ~H)) ^ ((q.y ^ ~ar) & H);
+    r.z = ((q.z | H) - (ar & ~H)) ^ ((q.z ^ ~ar) & H);
+    r.w = ((q.w | H) - (ar & ~H)) ^ ((q.w ^ ~ar) & H);
+    orow[v] = r;
+  }
 }
 
 // one thread per spectrum, channel-major [nchan][nspec] (Spectra layout)
@@ -502,7 +663,7 @@ __global__ __launch_bounds__(256) void k_smooth(const float* __restrict__ x, int
                                                 const float* __restrict__ padvals,
                                                 float* __restrict__ out, int64_t ld_out,
                                                 int64_t tiles) {
-  __shared__ float win[kSmoothLds];
+  extern __shared__ float win[];  // 1024 + w - 1 floats (sized by the launcher)
   const int64_t c = blockIdx.x / tiles, tile = blockIdx.x % tiles;
   const float* row = x + c * ld;
   const float pad = (pad_mode == PDD_PAD_VALUE) ? padvals[c] : 0.f;
@@ -571,6 +732,84 @@ __global__ __launch_bounds__(256) void k_zdm_ds(const T* __restrict__ in, int64_
   }
 }
 
+// Vectorised streaming prologue for 16-B aligned rows (nchan*sizeof(T) a
+// multiple of 16).  Spectrum means: one wave per spectrum, 16-byte loads,
+// exact integer (8/16-bit) or float64 (float32) sums.
+template <typename T>
+__global__ __launch_bounds__(256) void k_spectrum_mean_vec(const T* __restrict__ in, int64_t nspec,
+                                                           int64_t nchan, int64_t ld,
+                                                           double* __restrict__ mean) {
+  constexpr int VEC = 16 / sizeof(T);
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (s >= nspec) return;
+  const uint4* row = reinterpret_cast<const uint4*>(in + s * ld);
+  const int64_t nv = nchan / VEC;
+  double acc = 0.0;
+  for (int64_t v = lane; v < nv; v += 64) {
+    union { uint4 q; T e[VEC]; } u;
+    u.q = row[v];
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) acc += (double)u.e[e];
+    } else {
+      uint32_t p = 0;  // <= 8 x 65535: exact in 32 bits
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) p += (uint32_t)u.e[e];
+      acc += (double)p;
+    }
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) mean[s] = acc / (double)nchan;
+}
+
+// Fused corner turn + zero-DM (float mode) + downsample, one block = 64
+// outputs (64*f spectra) x 8*VEC channels: each thread sums f 16-byte rows of
+// VEC channels (in the order of k_zdm_ds) into the LDS tile, then every wave
+// writes whole 64-output channel rows.
+template <typename T>
+__global__ __launch_bounds__(256) void k_zdm_ds_vec(const T* __restrict__ in, int64_t nspec,
+                                                    int64_t nchan, int64_t ld,
+                                                    const double* __restrict__ mean, int f,
+                                                    float* __restrict__ out, int64_t ld_out,
+                                                    int64_t nout, int64_t tiles_c) {
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int TC = 8 * VEC;
+  __shared__ float tile[TC][65];
+  const int64_t tj = blockIdx.x / tiles_c, tc = blockIdx.x % tiles_c;
+  const int64_t j0 = tj * 64, c0 = tc * TC;
+  const int seg = threadIdx.x & 7, r0 = threadIdx.x >> 3;
+  const int64_t c = c0 + seg * VEC;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int jl = r0 + 32 * pass;
+    const int64_t j = j0 + jl;
+    float acc[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc[e] = 0.f;
+    if (j < nout && c < nchan) {
+      for (int k = 0; k < f; ++k) {
+        const int64_t t = j * f + k;
+        union { uint4 q; T e[VEC]; } u;
+        u.q = *reinterpret_cast<const uint4*>(in + t * ld + c);
+        const double m = mean ? mean[t] : 0.0;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[e] += (float)((double)u.e[e] - m);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) tile[seg * VEC + e][jl] = acc[e];
+  }
+  __syncthreads();
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t j = j0 + tx;
+#pragma unroll 4
+  for (int i = ty; i < TC; i += 4) {
+    const int64_t cc = c0 + i;
+    if (j < nout && cc < nchan) out[cc * ld_out + j] = tile[i][tx];
+  }
+}
+
 static int grid_1d(int64_t n, int per_block = 256) {
   int64_t g = cdiv(n, per_block);
   if (g > 2048 * 8) g = 2048 * 8;
@@ -607,7 +846,19 @@ int pdd_corner_turn(const void* in, int in_dtype, int64_t nspec, int64_t nchan, 
 #define CT(IT, OT)                                                                           \
   k_corner_turn<IT, OT><<<(unsigned)blocks, 256, 0, s>>>((const IT*)in, nspec, nchan, ld_in, \
                                                          (OT*)out, ld_out, tiles_c)
-  if (out_dtype == PDD_F32) {
+  const int64_t es = in_dtype == PDD_U8 ? 1 : (in_dtype == PDD_U16 ? 2 : 4);
+  if (out_dtype == PDD_F32 && (uintptr_t)in % 16 == 0 && (ld_in * es) % 16 == 0 &&
+      (nchan * es) % 16 == 0 && (in_dtype == PDD_U8 || in_dtype == PDD_U16 || in_dtype == PDD_F32)) {
+    const int64_t tcv = cdiv(nchan, 8 * (16 / es));
+    const int64_t bv = cdiv(nspec, 64) * tcv;
+#define CV(IT)                                                                                \
+  k_corner_turn_vec<IT><<<(unsigned)bv, 256, 0, s>>>((const IT*)in, nspec, nchan, ld_in,       \
+                                                    (float*)out, ld_out, tcv)
+    if (in_dtype == PDD_U8) CV(uint8_t);
+    else if (in_dtype == PDD_U16) CV(uint16_t);
+    else CV(float);
+#undef CV
+  } else if (out_dtype == PDD_F32) {
     if (in_dtype == PDD_U8) CT(uint8_t, float);
     else if (in_dtype == PDD_U16) CT(uint16_t, float);
     else if (in_dtype == PDD_F32) CT(float, float);
@@ -694,9 +945,22 @@ int pdd_shift_group_sum(const float* x, int64_t C, int64_t N, int64_t ld, const 
               "pdd_shift_group_sum: bad pad mode %d", pad_mode);
   if (C == 0 || n_out == 0) return 0;
   const int64_t tiles = cdiv(n_out, 256);
-  PDD_REQUIRE(nsub * tiles < (1ll << 31), "pdd_shift_group_sum: too large");
-  k_shift_group_sum<<<(unsigned)(nsub * tiles), 256, 0, as_stream(stream)>>>(
-      x, N, ld, bins, pad_mode, padvals, C / nsub, out, ld_out, n_out, tiles);
+  const int64_t cps = C / nsub;
+  // channel slices: enough workgroups to fill 256 CUs with 8-wave blocks
+  int64_t csplit = std::max<int64_t>(1, std::min<int64_t>(cdiv(2048, nsub * tiles),
+                                                          cps / (4 * kGsWaves)));
+  PDD_REQUIRE(csplit * nsub * tiles < (1ll << 31), "pdd_shift_group_sum: too large");
+  hipStream_t st = as_stream(stream);
+  double* part = nullptr;
+  if (csplit > 1)
+    PDD_HIP(hipMallocAsync((void**)&part, (size_t)(csplit * nsub * n_out) * sizeof(double), st));
+  k_shift_group_sum<<<(unsigned)(csplit * nsub * tiles), kGsWaves * 64, 0, st>>>(
+      x, N, ld, bins, pad_mode, padvals, cps, csplit, out, part, ld_out, n_out, tiles, nsub);
+  if (csplit > 1) {
+    k_group_sum_reduce<<<(unsigned)cdiv(nsub * n_out, 256), 256, 0, st>>>(part, csplit, nsub,
+                                                                          n_out, out, ld_out);
+    (void)hipFreeAsync(part, st);
+  }
   PDD_LAUNCHED();
   return 0;
 }
@@ -710,8 +974,12 @@ int pdd_downsample(const float* x, int64_t C, int64_t N, int64_t ld, int64_t fac
   if (C == 0 || nout == 0) return 0;
   const int64_t tiles = cdiv(nout, 256);
   PDD_REQUIRE(C * tiles < (1ll << 31), "pdd_downsample: too large");
-  k_downsample<<<(unsigned)(C * tiles), 256, 0, as_stream(stream)>>>(x, ld, factor, nout, out,
-                                                                     ld_out, tiles);
+  if (factor % 4 == 0 && (uintptr_t)x % 16 == 0 && ld % 4 == 0)
+    k_downsample_v4<<<(unsigned)(C * tiles), 256, 0, as_stream(stream)>>>(x, ld, factor, nout,
+                                                                          out, ld_out, tiles);
+  else
+    k_downsample<<<(unsigned)(C * tiles), 256, 0, as_stream(stream)>>>(x, ld, factor, nout, out,
+                                                                       ld_out, tiles);
   PDD_LAUNCHED();
   return 0;
 }
@@ -752,11 +1020,18 @@ int pdd_zero_dm(const void* in, int dtype, int64_t nspec, int64_t nchan, int64_t
     const int64_t g = cdiv(nspec, 4);
     PDD_REQUIRE(g < (1ll << 31), "pdd_zero_dm: too large");
 #define ZT(T) k_zero_dm_tm<T><<<(unsigned)g, 256, 0, s>>>((const T*)in, nspec, nchan, ld, (T*)out, ld_out)
-    if (dtype == PDD_U8) ZT(uint8_t);
+#define ZV(T) k_zero_dm_tm_vec<T><<<(unsigned)g, 256, 0, s>>>((const T*)in, nspec, nchan, ld, (T*)out, ld_out)
+    const int64_t es = dtype == PDD_U8 ? 1 : (dtype == PDD_U16 ? 2 : 4);
+    const bool vec = es < 4 && ((uintptr_t)in | (uintptr_t)out) % 16 == 0 &&
+                     (nchan * es) % 16 == 0 && (ld * es) % 16 == 0 && (ld_out * es) % 16 == 0;
+    if (dtype == PDD_U8 && vec) ZV(uint8_t);
+    else if (dtype == PDD_U16 && vec) ZV(uint16_t);
+    else if (dtype == PDD_U8) ZT(uint8_t);
     else if (dtype == PDD_U16) ZT(uint16_t);
     else if (dtype == PDD_F32) ZT(float);
     else PDD_REQUIRE(false, "pdd_zero_dm: bad dtype %d", dtype);
 #undef ZT
+#undef ZV
   } else if (layout == PDD_LAYOUT_CHAN_MAJOR) {
     PDD_REQUIRE(ld >= nspec && ld_out >= nspec, "pdd_zero_dm: bad ld");
     const int64_t g = cdiv(nspec, 256);
@@ -832,8 +1107,9 @@ int pdd_smooth(const float* x, int64_t C, int64_t N, int64_t ld, int64_t width, 
   if (C == 0) return 0;
   const int64_t tiles = cdiv(N, 1024);
   PDD_REQUIRE(C * tiles < (1ll << 31), "pdd_smooth: too large");
-  k_smooth<<<(unsigned)(C * tiles), 256, 0, as_stream(stream)>>>(x, N, ld, width, pad_mode, padvals,
-                                                                 out, ld_out, tiles);
+  const size_t lds = (size_t)(1024 + width - 1) * sizeof(float);  // <= 32 KiB
+  k_smooth<<<(unsigned)(C * tiles), 256, lds, as_stream(stream)>>>(x, N, ld, width, pad_mode,
+                                                                   padvals, out, ld_out, tiles);
   PDD_LAUNCHED();
   return 0;
 }
@@ -860,11 +1136,27 @@ int pdd_zdm_downsample(const void* in, int dtype, int64_t nspec, int64_t nchan, 
     k_zdm_ds<T><<<(unsigned)blocks, 256, 0, s>>>((const T*)in, nspec, nchan, ld, mean,          \
                                                  (int)factor, out, ld_out, tiles_c);            \
   } while (0)
-  if (dtype == PDD_U8) ZD(uint8_t);
+#define ZV(T)                                                                                   \
+  do {                                                                                          \
+    if (zero_dm)                                                                                \
+      k_spectrum_mean_vec<T><<<(unsigned)cdiv(nspec, 4), 256, 0, s>>>((const T*)in, nspec,     \
+                                                                       nchan, ld, mean);        \
+    const int64_t tcv = cdiv(nchan, 8 * (16 / (int64_t)sizeof(T)));                            \
+    k_zdm_ds_vec<T><<<(unsigned)(cdiv(nout, 64) * tcv), 256, 0, s>>>(                           \
+        (const T*)in, nspec, nchan, ld, mean, (int)factor, out, ld_out, nout, tcv);             \
+  } while (0)
+  const int64_t es = dtype == PDD_U8 ? 1 : (dtype == PDD_U16 ? 2 : 4);
+  const int64_t nout = nspec / factor;
+  const bool vec = (uintptr_t)in % 16 == 0 && (ld * es) % 16 == 0 && (nchan * es) % 16 == 0;
+  if (vec && dtype == PDD_U8) ZV(uint8_t);
+  else if (vec && dtype == PDD_U16) ZV(uint16_t);
+  else if (vec && dtype == PDD_F32) ZV(float);
+  else if (dtype == PDD_U8) ZD(uint8_t);
   else if (dtype == PDD_U16) ZD(uint16_t);
   else if (dtype == PDD_F32) ZD(float);
   else PDD_REQUIRE(false, "pdd_zdm_downsample: bad dtype %d", dtype);
 #undef ZD
+#undef ZV
   const hipError_t e = hipGetLastError();
   if (mean) (void)hipFreeAsync(mean, s);
   PDD_REQUIRE(e == hipSuccess, "pdd_zdm_downsample: launch failed: %s", hipGetErrorString(e));
