@@ -339,25 +339,45 @@ __global__ __launch_bounds__(256) void k_downsample_v4(const float* __restrict__
 // 8-bit input (a Spectra's raw bytes): integer sums (exact), one 16-byte load
 // per lane when the factor divides 16 and the rows are 16-B aligned -- a
 // quarter of the float32 image's bytes (DDplan executor, spectra.py:329-351)
+template <int F>
 __global__ __launch_bounds__(256) void k_downsample_u8v(const uint8_t* __restrict__ x, int64_t ld,
-                                                        int factor, int64_t nvec,
-                                                        float* __restrict__ out, int64_t ld_out,
-                                                        int64_t nout, int64_t tiles) {
+                                                        int64_t nvec, float* __restrict__ out,
+                                                        int64_t ld_out, int64_t nout,
+                                                        int64_t tiles, bool vstore) {
+  constexpr int PER = 16 / F;  // outputs per 16-byte vector
   const int64_t c = blockIdx.x / tiles, tile = blockIdx.x % tiles;
   const int64_t v = tile * 256 + threadIdx.x;  // 16-byte vector index in the row
   if (v >= nvec) return;
   const uint4 q = *reinterpret_cast<const uint4*>(x + c * ld + v * 16);
   const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-  const int per = 16 / factor;  // outputs per vector
-  float* o = out + c * ld_out + v * per;
-  for (int k = 0; k < per; ++k) {
+  float r[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
     uint32_t s = 0;
-    for (int b = 0; b < factor; ++b) {
-      const int e = k * factor + b;
+#pragma unroll
+    for (int b = 0; b < F; ++b) {
+      const int e = k * F + b;
       s += (w[e >> 2] >> (8 * (e & 3))) & 0xffu;
     }
-    if (v * per + k < nout) o[k] = (float)s;
+    r[k] = (float)s;
   }
+  float* o = out + c * ld_out + v * PER;
+  if constexpr (PER >= 4) {
+    if (vstore && v * PER + PER <= nout) {
+#pragma unroll
+      for (int k = 0; k < PER; k += 4)
+        *reinterpret_cast<float4*>(o + k) = make_float4(r[k], r[k + 1], r[k + 2], r[k + 3]);
+      return;
+    }
+  } else if constexpr (PER == 2) {
+    if (vstore && v * PER + PER <= nout) {
+      *reinterpret_cast<float2*>(o) = make_float2(r[0], r[1]);
+      return;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k)
+    if (v * PER + k < nout) o[k] = r[k];
 }
 
 __global__ __launch_bounds__(256) void k_downsample_u8(const uint8_t* __restrict__ x, int64_t ld,
@@ -644,7 +664,7 @@ __global__ __launch_bounds__(256) void k_masked_fill(const float* __restrict__ x
 
 // Boxcar smooth: out[c][t] = (1/sqrt(w)) * sum_{j = t - w/2}^{t + (w-1)/2} P(c, j)
 // with P the padded channel (value pad, or wrap for PDD_PAD_ROTATE).  The
-// window of one 1024-output tile is staged in LDS (w <= kSmoothLds - 1023);
+// window of one 4096-output tile is staged in LDS (w <= kSmoothLds - 1023);
 // sums in float64.
 constexpr int kSmoothLds = 8192;
 
@@ -658,30 +678,67 @@ __device__ __forceinline__ float smooth_src(const float* row, int64_t j, int64_t
   return pad;
 }
 
+constexpr int kSmoothOpt = 16;                 // outputs per thread
+constexpr int kSmoothTile = 256 * kSmoothOpt;  // outputs per workgroup
 __global__ __launch_bounds__(256) void k_smooth(const float* __restrict__ x, int64_t N, int64_t ld,
                                                 int64_t w, int pad_mode,
                                                 const float* __restrict__ padvals,
                                                 float* __restrict__ out, int64_t ld_out,
                                                 int64_t tiles) {
-  extern __shared__ float win[];  // 1024 + w - 1 floats (sized by the launcher)
+  extern __shared__ float win[];  // kSmoothTile + w floats (sized by the launcher)
   const int64_t c = blockIdx.x / tiles, tile = blockIdx.x % tiles;
   const float* row = x + c * ld;
   const float pad = (pad_mode == PDD_PAD_VALUE) ? padvals[c] : 0.f;
-  const int64_t t0 = tile * 1024;
+  const int64_t t0 = tile * kSmoothTile;
   const int64_t j0 = t0 - w / 2;
-  const int64_t nw = 1024 + w - 1;
-  for (int64_t i = threadIdx.x; i < nw; i += 256) win[i] = smooth_src(row, j0 + i, N, pad_mode, pad);
+  const int64_t nw = kSmoothTile + w - 1;
+  {
+    // all of a thread's window loads in flight before its LDS stores
+    float v[kSmoothOpt];
+#pragma unroll
+    for (int q = 0; q < kSmoothOpt; ++q)
+      v[q] = smooth_src(row, j0 + q * 256 + threadIdx.x, N, pad_mode, pad);
+#pragma unroll
+    for (int q = 0; q < kSmoothOpt; ++q) win[q * 256 + threadIdx.x] = v[q];
+    for (int64_t i = kSmoothTile + threadIdx.x; i < nw; i += 256)
+      win[i] = smooth_src(row, j0 + i, N, pad_mode, pad);
+    if (threadIdx.x == 0) win[nw] = 0.f;  // the spare slot the sliding window reads last
+  }
   __syncthreads();
   const double k = 1.0 / sqrt((double)w);
+  // thread = kSmoothOpt consecutive outputs; each window summed from its first
+  // sample in order (the arithmetic of one output is unchanged), the windows
+  // share a sliding register window: w + kSmoothOpt - 1 LDS reads
+  const int o = kSmoothOpt * threadIdx.x;
+  float r[kSmoothOpt];
+  double sm[kSmoothOpt];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int64_t o = q * 256 + threadIdx.x;
-    if (t0 + o >= N) continue;
-    double s = 0.0;
-    for (int64_t i = 0; i < w; ++i) s += (double)win[o + i];
-    out[c * ld_out + t0 + o] = (float)(s * k);
+  for (int q = 0; q < kSmoothOpt; ++q) {
+    r[q] = win[o + q];
+    sm[q] = 0.0;
+  }
+  for (int64_t i = 0; i < w; ++i) {
+#pragma unroll
+    for (int q = 0; q < kSmoothOpt; ++q) sm[q] += (double)r[q];
+#pragma unroll
+    for (int q = 0; q < kSmoothOpt - 1; ++q) r[q] = r[q + 1];
+    r[kSmoothOpt - 1] = win[o + kSmoothOpt + i];
+  }
+  const int64_t t = t0 + o;
+  float* orow = out + c * ld_out;
+  if (t + kSmoothOpt <= N && (((uintptr_t)(orow + t)) & 15) == 0) {
+#pragma unroll
+    for (int q = 0; q < kSmoothOpt; q += 4)
+      *reinterpret_cast<float4*>(orow + t + q) =
+          make_float4((float)(sm[q] * k), (float)(sm[q + 1] * k), (float)(sm[q + 2] * k),
+                      (float)(sm[q + 3] * k));
+  } else {
+#pragma unroll
+    for (int q = 0; q < kSmoothOpt; ++q)
+      if (t + q < N) orow[t + q] = (float)(sm[q] * k);
   }
 }
+
 
 // ---------------------------------------------------------------- streaming prologue
 // Per-spectrum channel mean (float64) of a time-major block.
@@ -998,8 +1055,16 @@ int pdd_downsample_u8(const uint8_t* x, int64_t C, int64_t N, int64_t ld, int64_
     PDD_REQUIRE(nvec * 16 <= ld, "pdd_downsample_u8: row padding");
     const int64_t tiles = cdiv(nvec, 256);
     PDD_REQUIRE(C * tiles < (1ll << 31), "pdd_downsample_u8: too large");
-    k_downsample_u8v<<<(unsigned)(C * tiles), 256, 0, s>>>(x, ld, (int)factor, nvec, out, ld_out,
-                                                          nout, tiles);
+    const int per = (int)(16 / factor);
+    const bool vstore = (uintptr_t)out % (per >= 4 ? 16 : 8) == 0 &&
+                        ld_out % (per >= 4 ? 4 : 2) == 0 && per >= 2;
+#define DV(F_) k_downsample_u8v<F_><<<(unsigned)(C * tiles), 256, 0, s>>>(x, ld, nvec, out, ld_out, nout, tiles, vstore)
+    if (factor == 1) DV(1);
+    else if (factor == 2) DV(2);
+    else if (factor == 4) DV(4);
+    else if (factor == 8) DV(8);
+    else DV(16);
+#undef DV
   } else {
     const int64_t tiles = cdiv(nout, 256);
     PDD_REQUIRE(C * tiles < (1ll << 31), "pdd_downsample_u8: too large");
@@ -1105,9 +1170,9 @@ int pdd_smooth(const float* x, int64_t C, int64_t N, int64_t ld, int64_t width, 
               "pdd_smooth: bad pad mode %d", pad_mode);
   PDD_REQUIRE(pad_mode != PDD_PAD_ROTATE || width <= N, "pdd_smooth: wrap needs width <= N");
   if (C == 0) return 0;
-  const int64_t tiles = cdiv(N, 1024);
+  const int64_t tiles = cdiv(N, kSmoothTile);
   PDD_REQUIRE(C * tiles < (1ll << 31), "pdd_smooth: too large");
-  const size_t lds = (size_t)(1024 + width - 1) * sizeof(float);  // <= 32 KiB
+  const size_t lds = (size_t)(kSmoothTile + width) * sizeof(float);  // <= 48 KiB
   k_smooth<<<(unsigned)(C * tiles), 256, lds, as_stream(stream)>>>(x, N, ld, width, pad_mode,
                                                                    padvals, out, ld_out, tiles);
   PDD_LAUNCHED();
