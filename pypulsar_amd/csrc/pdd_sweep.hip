@@ -1893,7 +1893,8 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
               "pdd_sweep_plan_create: bad extents D=%lld C=%lld", (long long)D, (long long)C);
   PDD_REQUIRE(dtype == PDD_F32 || dtype == PDD_U8, "pdd_sweep_plan_create: dtype must be F32 or U8");
   const Variant* cands = dtype == PDD_U8 ? kU8Variants : kF32Variants;
-  const int ncand = dtype == PDD_U8 ? 11 : 15;
+  const int ncand = dtype == PDD_U8 ? (int)(sizeof(kU8Variants) / sizeof(Variant))
+                                    : (int)(sizeof(kF32Variants) / sizeof(Variant));
 
   const int fv = forced_variant();
   for (int vi = (fv >= 0 && fv < ncand) ? fv : 0; vi < ncand; ++vi) {
