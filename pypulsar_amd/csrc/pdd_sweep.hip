@@ -1327,7 +1327,13 @@ __host__ __device__ constexpr int il_meta_bytes(int nlw, int nbuf, int cc, int d
 // dbg bit 4: plain XCD-contiguous order (trial block fastest); bit 5: natural.
 __device__ __forceinline__ void il_tile_of(int bid, int n_tblk, int n_dblk, int dbg, int& dblk,
                                            int& tblk) {
-  constexpr int GT = 8, GJ = 4;
+#ifndef PDD_IL_GT
+#define PDD_IL_GT 8
+#endif
+#ifndef PDD_IL_GJ
+#define PDD_IL_GJ 4
+#endif
+  constexpr int GT = PDD_IL_GT, GJ = PDD_IL_GJ;
   const int total = n_tblk * n_dblk;
   if (dbg & 32) {
     dblk = bid % n_dblk;
