@@ -1226,25 +1226,33 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_ws(
 // dedicated loader waves, and every compute-wave ds_read_b128 at a trial's
 // (wave-uniform) shift returns 4 samples -- one per quarter -- that share it.
 // Output (trial d, element e, quarter k) is plane[d][t_base + e + k*Qs].
+// Each thread writes kIlPer elements 256 apart, issuing all their loads
+// before any store (memory-level parallelism for the strided quarter reads).
+constexpr int kIlPer = 4;
 template <typename InT>
 __global__ __launch_bounds__(256) void k_interleave(const InT* __restrict__ x, int64_t ld, int64_t N,
                                                     int64_t base, int64_t Qs, int64_t nR,
                                                     int pad_mode, const float* __restrict__ padvals,
                                                     float4* __restrict__ R) {
   const int c = blockIdx.y;
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= nR) return;
+  const int64_t j0 = (int64_t)blockIdx.x * (256 * kIlPer) + threadIdx.x;
   const InT* row = x + (int64_t)c * ld;
   const float pv = (pad_mode == PDD_PAD_VALUE) ? padvals[c] : 0.f;
-  float v[4];
+  float v[kIlPer][4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int64_t s = base + j + k * Qs;
-    if (s >= 0 && s < N) v[k] = (float)row[s];
-    else if (pad_mode == PDD_PAD_ROTATE) v[k] = (float)row[wrap_mod(s, N)];
-    else v[k] = pv;
+  for (int i = 0; i < kIlPer; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t s = base + j0 + i * 256 + k * Qs;
+      if (s >= 0 && s < N) v[i][k] = (float)row[s];
+      else if (pad_mode == PDD_PAD_ROTATE) v[i][k] = (float)row[wrap_mod(s, N)];
+      else v[i][k] = pv;
+    }
+#pragma unroll
+  for (int i = 0; i < kIlPer; ++i) {
+    const int64_t j = j0 + i * 256;
+    if (j < nR) R[(int64_t)c * nR + j] = make_float4(v[i][0], v[i][1], v[i][2], v[i][3]);
   }
-  R[(int64_t)c * nR + j] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
 // u16 eighths for 8-bit data: R[c][j] = 8 samples X(c, b + j + k*Qs), k < 8,
@@ -1256,20 +1264,26 @@ __global__ __launch_bounds__(256) void k_interleave_u16(const uint8_t* __restric
                                                         const float* __restrict__ padvals,
                                                         uint4* __restrict__ R) {
   const int c = blockIdx.y;
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= nR) return;
+  const int64_t j0 = (int64_t)blockIdx.x * (256 * kIlPer) + threadIdx.x;
   const uint8_t* row = x + (int64_t)c * ld;
   const uint32_t pv = (pad_mode == PDD_PAD_VALUE) ? (uint32_t)padvals[c] : 0u;
-  uint32_t v[8];
+  uint32_t v[kIlPer][8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int64_t s = base + j + k * Qs;
-    if (s >= 0 && s < N) v[k] = row[s];
-    else if (pad_mode == PDD_PAD_ROTATE) v[k] = row[wrap_mod(s, N)];
-    else v[k] = pv;
+  for (int i = 0; i < kIlPer; ++i)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t s = base + j0 + i * 256 + k * Qs;
+      if (s >= 0 && s < N) v[i][k] = row[s];
+      else if (pad_mode == PDD_PAD_ROTATE) v[i][k] = row[wrap_mod(s, N)];
+      else v[i][k] = pv;
+    }
+#pragma unroll
+  for (int i = 0; i < kIlPer; ++i) {
+    const int64_t j = j0 + i * 256;
+    if (j < nR)
+      R[(int64_t)c * nR + j] = make_uint4(v[i][0] | (v[i][1] << 16), v[i][2] | (v[i][3] << 16),
+                                          v[i][4] | (v[i][5] << 16), v[i][6] | (v[i][7] << 16));
   }
-  R[(int64_t)c * nR + j] = make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16),
-                                      v[6] | (v[7] << 16));
 }
 
 // n DMAs of 64 elements (1 KiB) each, q = first, first + step, ...
@@ -1853,7 +1867,7 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
     const int64_t cnt = std::min(seg, n_out - t_base);
     const int64_t Qs = cdiv(cdiv(cnt, SP), Tq) * Tq;
     const int64_t nR = Qs + (hi - lo) + 64;
-    dim3 g1((unsigned)cdiv(nR, 256), (unsigned)C);
+    dim3 g1((unsigned)cdiv(nR, 256 * kIlPer), (unsigned)C);
     if (u16)
       hipLaunchKernelGGL(k_interleave_u16, g1, dim3(256), 0, st, (const uint8_t*)x, ld, N,
                          t_base + lo, Qs, nR, pad_mode, padvals, (uint4*)R);
