@@ -1,28 +1,39 @@
 #!/usr/bin/env python
-"""Benchmark: the batched brute-force DM sweep (BASELINE.json configs[1]).
+"""Benchmark: the batched brute-force DM sweep.
 
-Workload (one "step" = one sweep of one resident block):
-    C = 1024 channels x N = 2^20 samples x D = 1024 DM trials (0-1000 pc/cc,
-    uniform), 64 us sampling, 1250-1550 MHz band, float32 input (default) or
-    8-bit (--dtype u8), trim=True (plane width N - max delay = 1,034,083).
-Metric: DM-trial samples*channels per second (whole job), = D * n_out * C
-per step per rank / time.
+Default workload = BASELINE.json configs[3], the configuration the metric is
+quoted on: ONE 8-bit filterbank block of C = 4096 channels x N = 2^22 samples
+swept over D = 4096 DM trials (0-1000 pc/cc, uniform), 64 us sampling,
+1250-1550 MHz band, trim=True (plane width N - max delay = 4,179,800),
+DM-sharded across the ranks (pypulsar_amd.sharding.DMShardedSweep):
+    * the block is resident in HBM in file order (time-major), each rank
+      holding its 1/N slice of every time batch (its own H2D share);
+    * one step = RCCL all-gathers of the time batches over xGMI, batch k+1's
+      gather overlapping batch k's corner turn + sweep, + the sweep of the
+      rank's DM slice (balanced by DDplan work fraction, DDplan2b.py:272-273);
+      planes stay resident per rank ("strong" scaling: total work fixed);
+    * at N = 1 the same path runs without collectives.
+Metric: DM-trial samples*channels per second of the whole job
+= D * n_out * C per step / step time (max over ranks).
+Other workloads: --config config2 (BASELINE configs[1], 1024 x 2^20 x 1024,
+float32, time-block mode), northstar (4096 x 2^22 x 2048), stream
+(configs[4]), subband (configs[2]), search, ops (incl. configs[0]).
 
-Multi-GPU (torchrun, one rank per GPU): time-block sharding -- every rank
-sweeps its OWN block (seeded by rank) over the full DM grid, no data-path
-collective ("scaling": "weak"); --mode dmshard instead shards ONE block's DM
-grid ("strong"): each step all-gathers the block from the ranks' 1/N slices
-over RCCL, corner-turns it and sweeps the rank's DM slice
-(pypulsar_amd.sharding; planes stay resident for a downstream search).
+Multi-GPU: `--gpus N` without WORLD_SIZE in the environment starts N ranks
+itself (torch.distributed.run on 127.0.0.1, before any GPU call); under
+torchrun it uses RANK/LOCAL_RANK/WORLD_SIZE.
 
 Timing: W untimed warm-up steps, then exactly K steps bracketed by a barrier
-+ torch.cuda.synchronize(); the max over ranks is reported.  The sweep
-kernel's own duration is measured with HIP events on the stream it is
-launched on (torch's current stream) around every timed launch.
++ torch.cuda.synchronize(); the max over ranks is reported.  Inside the timed
+region every sweep-kernel launch is bracketed by its own HIP event pair on the
+stream it runs on (libpdd's event pool, no host syncs); roofline.achieved =
+algorithmic adds of those launches / their summed duration.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,15 +46,22 @@ sys.path.insert(0, ROOT)
 
 # MI355X peaks (MI355X_MICROARCH.md §Chip-level parameters)
 PEAK_HBM_GBS = 8000.0
-PEAK_F32_TFLOPS = 157.3   # FP32 vector peak == FP32 dense MFMA peak on gfx950
-PEAK_ADD_T = 78.6         # pure adds: 256 CU x 2.4 GHz x 128 (v_pk_add_f32), SURVEY.md §8(d)
+PEAK_ADD_T = 78.6   # VALU adds: 256 CU x 2.4 GHz x 128 (v_pk_add_f32 / two u16 lanes per v_add_u32)
+CLK_GHZ = 2.4
+N_CU = 256
 
 CONFIGS = {
-    # BASELINE.json configs[1]
-    "config2": dict(C=1024, N=1 << 20, D=1024, dm_lo=0.0, dm_hi=1000.0),
+    # BASELINE.json configs[3] (the metric's configuration): DM-sharded node sweep
+    "config3": dict(C=4096, N=1 << 22, D=4096, dm_lo=0.0, dm_hi=1000.0, dtype="u8",
+                    mode="dmshard", cpu=(4096, 1 << 17, 12), baseline_index=3),
+    # BASELINE.json configs[1]: single-GPU brute-force sweep, float32
+    "config2": dict(C=1024, N=1 << 20, D=1024, dm_lo=0.0, dm_hi=1000.0, dtype="f32",
+                    mode="timeblock", cpu=(1024, 1 << 20, 3), baseline_index=1),
     # north-star single-GPU target (4096 ch x 2048 DM x 2^22)
-    "northstar": dict(C=4096, N=1 << 22, D=2048, dm_lo=0.0, dm_hi=1000.0),
-    "small": dict(C=256, N=1 << 18, D=256, dm_lo=0.0, dm_hi=500.0),
+    "northstar": dict(C=4096, N=1 << 22, D=2048, dm_lo=0.0, dm_hi=1000.0, dtype="u8",
+                      mode="dmshard", cpu=(4096, 1 << 17, 12), baseline_index=None),
+    "small": dict(C=256, N=1 << 18, D=256, dm_lo=0.0, dm_hi=500.0, dtype="f32",
+                  mode="timeblock", cpu=(256, 1 << 18, 8), baseline_index=None),
     # BASELINE.json configs[4]: streaming u8 blocks, zero-DM + ds 2 + 2048 DMs
     "stream": dict(C=4096, N=1 << 18, D=2048, dm_lo=0.0, dm_hi=1000.0, ds=2),
     # BASELINE.json configs[2]: two-stage subband sweep over a DDplan2b grid
@@ -56,30 +74,40 @@ CONFIGS = {
 }
 
 
+def log(*a):
+    print("[bench %s]" % time.strftime("%H:%M:%S"), *a, file=sys.stderr, flush=True)
+
+
 def band(C, lo=1250.0, hi=1550.0):
     foff = -(hi - lo) / C
     return (hi + foff / 2.0) + foff * np.arange(C)
 
 
-def synth_block(C, N, seed, dtype, device):
-    """uint8 clip(round(N(128, 16))) filterbank block, generated on the device."""
+def synth_block(C, N, seed, dtype, device, rows_per_chunk=1 << 26):
+    """uint8 clip(round(N(128, 16))) filterbank block [C, N], generated on the
+    device in row chunks (bounded float32 temporaries)."""
     g = torch.Generator(device=device)
     g.manual_seed(seed)
-    x = torch.empty((C, N), dtype=torch.float32, device=device)
-    x.normal_(128.0, 16.0, generator=g)
-    x = x.round_().clamp_(0, 255)
-    return x.to(torch.uint8) if dtype == "u8" else x
+    out = torch.empty((C, N), dtype=torch.uint8 if dtype == "u8" else torch.float32,
+                      device=device)
+    step = max(1, rows_per_chunk // max(N, 1))
+    for r in range(0, C, step):
+        x = torch.empty((min(step, C - r), N), dtype=torch.float32, device=device)
+        x.normal_(128.0, 16.0, generator=g)
+        x = x.round_().clamp_(0, 255)
+        out[r:r + x.shape[0]] = x.to(out.dtype)
+        del x
+    return out
 
 
-def cpu_baseline(cfg, ntrials, dt):
+def cpu_baseline(C, n, dms, ntrials, dt, full_N):
     """Oracle (NumPy restatement of Spectra.dedisperse + channel sum, C-order,
-    one core) on a bounded sample: ntrials full-length DM trials."""
+    one core) on a BOUNDED sample of the workload: ``ntrials`` DM trials of
+    the grid (spread over it) on a C x n block (n <= the workload's N)."""
     from oracle import spectra_oracle as orc
-    C, N = cfg["C"], cfg["N"]
     freqs = band(C)
     rng = np.random.default_rng(0)
-    x = np.clip(np.round(rng.normal(128, 16, (C, N))), 0, 255).astype(np.float64)
-    dms = np.linspace(cfg["dm_lo"], cfg["dm_hi"], cfg["D"])
+    x = np.clip(np.round(rng.normal(128, 16, (C, n))), 0, 255).astype(np.float64)
     pick = dms[np.linspace(0, len(dms) - 1, ntrials).astype(int)]
     work = 0
     t0 = time.perf_counter()
@@ -87,11 +115,12 @@ def cpu_baseline(cfg, ntrials, dt):
         d, _ = orc.dedisperse(x, freqs, dt, dm, padval=0, trim=True)
         s = orc.channel_sum(d)
         work += s.shape[0] * C
+        del d, s
     el = time.perf_counter() - t0
     res = dict(value=work / el, unit="samples*channels*DM/s", cores=1, kind="port",
-               sample="%d full-length DM trials (dedisperse(trim=True)+channel sum), "
-                      "%d ch x %d samples, float64 NumPy C-order, 1 thread, %.1f s"
-                      % (ntrials, C, N, el))
+               sample="%d DM trials of the grid (dedisperse(trim=True)+channel sum), "
+                      "%d ch x %d samples (workload: %d), float64 NumPy C-order, 1 thread, "
+                      "%.1f s" % (ntrials, C, n, full_N, el))
     res["cpu_model"] = _cpu_model()
     res["nproc"] = os.cpu_count()
     res["f_order_1core"] = _cpu_forder(x, freqs, dt, pick[-1], orc)
@@ -109,7 +138,7 @@ def _cpu_model():
     return None
 
 
-def _cpu_forder(x, freqs, dt, dm, orc, n=1 << 17):
+def _cpu_forder(x, freqs, dt, dm, orc, n=1 << 16):
     """One trial on the F-order layout get_spectra produces (filterbank.py:
     155-157 reshape + .T), where the reference's per-channel rotate walks
     strided rows: first ``n`` samples only, per unit."""
@@ -138,12 +167,12 @@ def _pool_task(args):
     return (c1 - c0) * n_keep
 
 
-def _cpu_pool(x, freqs, dt, dms, orc, workers=12, ntrials=16, cblk=32):
+def _cpu_pool(x, freqs, dt, dms, orc, workers=12, ntrials=16, cblk=64):
     """DM-parallel multiprocessing variant: ``workers``
-    forked processes over (DM, 32-channel block) tasks of ``ntrials``
-    full-length trials.  12, not the box's 16-CPU share: the forked children
-    inherit the parent's GPU file descriptors and the box limits how many
-    processes may hold the card."""
+    forked processes over (DM, channel block) tasks of ``ntrials`` trials.
+    12, not the box's 16-CPU share: the forked children inherit the parent's
+    GPU file descriptors and the box limits how many processes may hold the
+    card."""
     import multiprocessing as mp
     global _POOL_X
     _POOL_X = x
@@ -163,8 +192,9 @@ def _cpu_pool(x, freqs, dt, dms, orc, workers=12, ntrials=16, cblk=32):
         el = time.perf_counter() - t0
     _POOL_X = None
     return dict(value=work / el, cores=workers,
-                sample="%d full-length DM trials split into %d-channel blocks over %d forked "
-                       "processes, float64 NumPy C-order, %.1f s" % (ntrials, cblk, workers, el))
+                sample="%d DM trials on the same block split into %d-channel blocks over %d "
+                       "forked processes, float64 NumPy C-order, %.1f s" % (ntrials, cblk, workers,
+                                                                              el))
 
 
 def load_pmc(path, key):
@@ -176,16 +206,39 @@ def load_pmc(path, key):
         return None
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _maybe_spawn(args):
+    """`--gpus N` outside torchrun: start N ranks (one per GPU) with
+    torch.distributed.run before this process touches the GPU, and exit with
+    their status."""
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+               "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="config2", choices=sorted(CONFIGS))
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--config", default="config3", choices=sorted(CONFIGS))
     ap.add_argument("--block", type=int, default=None, help="stream: spectra per block")
-    ap.add_argument("--dtype", default="f32", choices=["f32", "u8"])
-    ap.add_argument("--mode", default="timeblock", choices=["timeblock", "dmshard"])
-    ap.add_argument("--cpu-trials", type=int, default=3)
+    ap.add_argument("--dtype", default=None, choices=["f32", "u8"])
+    ap.add_argument("--mode", default=None, choices=["timeblock", "dmshard"])
+    ap.add_argument("--batches", type=int, default=None,
+                    help="dmshard: time batches per step (default 1 on one GPU, 4 otherwise)")
+    ap.add_argument("--gather", action="store_true",
+                    help="dmshard: also gather every batch's plane rows to rank 0 (p2p)")
+    ap.add_argument("--cpu-trials", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true",
                     help="also time one PCIe-inclusive step: pinned host block -> H2D -> "
@@ -193,6 +246,7 @@ def main():
     ap.add_argument("--search", action="store_true",
                     help="stream: also boxcar-search every block (StreamingSearch)")
     args = ap.parse_args()
+    _maybe_spawn(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -208,9 +262,11 @@ def main():
     if world > 1:
         dist.barrier()
     g.build()
-    from pypulsar_amd.sweep import DMSweep
 
     cfg = CONFIGS[args.config]
+    if args.config in ("stream", "subband", "search", "ops"):
+        args.steps = 10 if args.steps is None else args.steps
+        args.warmup = 3 if args.warmup is None else args.warmup
     if args.config == "stream":
         return stream_bench(args, cfg, rank, world, dev)
     if args.config == "subband":
@@ -219,64 +275,68 @@ def main():
         return search_bench(args, cfg, rank, world, dev)
     if args.config == "ops":
         return ops_bench(args, cfg, rank, world, dev)
+    return sweep_bench(args, cfg, rank, world, dev)
+
+
+def sweep_bench(args, cfg, rank, world, dev):
+    from pypulsar_amd.sweep import DMSweep
+    from pypulsar_amd.sharding import DMShardedSweep, trial_work
+    big = cfg["C"] * cfg["N"] >= (1 << 34)
+    steps = args.steps if args.steps is not None else (5 if big else 10)
+    warmup = args.warmup if args.warmup is not None else (1 if big else 3)
     C, N, D = cfg["C"], cfg["N"], cfg["D"]
+    dtype = args.dtype or cfg["dtype"]
+    mode = args.mode or cfg["mode"]
     dt = 64e-6
     freqs = band(C)
     dms_all = np.linspace(cfg["dm_lo"], cfg["dm_hi"], D)
+    tdt = torch.uint8 if dtype == "u8" else torch.float32
+    nb = None
+    if mode == "dmshard":
+        nb = args.batches or (1 if world == 1 else 4)
+        # uniform grid = one DDstep at downsamp 1: every trial weighs 1/1
+        # (DDplan2b.py:272-273); DMShardedSweep balances the slices by it
+        ds = DMShardedSweep(dms_all, freqs, dt, N, dtype=tdt, n_batches=nb,
+                            work=trial_work(dms_all, 1), gather=args.gather, device=dev)
+        log("rank %d: DM slice [%d, %d) of %d, %d batch(es)" % (rank, ds.lo, ds.hi, D, nb))
+        # this rank's H2D share of every time batch, [nb, N/(nb*world), C],
+        # in file (time-major) order
+        n_r = N // (nb * world)
+        part = synth_block(nb * n_r, C, 1000 + rank, dtype, dev).view(nb, n_r, C)
+        sw, rows, n_out = ds.sw, ds.rows, ds.n_out
 
-    if args.mode == "timeblock":
-        dms = dms_all
-        x = synth_block(C, N, 1000 + rank, args.dtype, dev)
+        def step():
+            return ds(part)
     else:
-        # DM sharding (strong scaling): each rank holds 1/world of the
-        # time-major block; every step all-gathers it over RCCL, corner-turns
-        # it on the device and sweeps this rank's DM slice (sharding.py)
-        from pypulsar_amd import _lib
-        from pypulsar_amd._lib import call, ptr, stream_ptr
-        from pypulsar_amd.sharding import allgather_block, dm_slices
-        lo, hi = dm_slices(D, world)[rank]
-        dms = dms_all[lo:hi]
-        assert N % world == 0
-        part = synth_block(N // world, C, 1000 + rank, args.dtype, dev)  # [N/world, C]
-        x = torch.empty((C, N), dtype=part.dtype, device=dev)
-        code = _lib.U8 if args.dtype == "u8" else _lib.F32
-    sw = DMSweep(dms, freqs, dt, dtype=args.dtype)
-    # plane width of the full grid (trim=True): identical on every rank
-    full_max = int(DMSweep(dms_all[-1:], freqs, dt).max_bin)
-    n_out = N - max(0, full_max)
-    plane = torch.empty((len(dms), n_out), dtype=torch.float32, device=dev)
+        x = synth_block(C, N, 1000 + rank, dtype, dev)
+        sw = DMSweep(dms_all, freqs, dt, dtype=dtype)
+        rows, n_out = D, sw.n_out(N)
+        plane = torch.empty((D, n_out), dtype=torch.float32, device=dev)
 
-    def step():
-        if args.mode != "timeblock":
-            blk = allgather_block(part) if world > 1 else part
-            call("pdd_corner_turn", ptr(blk), code, N, C, C, ptr(x), code, N, stream_ptr())
-        return sw(x, out=plane)
-
-    for _ in range(args.warmup):
+        def step():
+            return sw(x, out=plane)
+    log("rank %d: block synthesised; warm-up x%d" % (rank, warmup))
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if sw is not None:
+        sw.set_timing(True)  # event pair per sweep launch, no host syncs
+    log("rank %d: timing %d steps" % (rank, steps))
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(steps):
         step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    # the sweep kernel's own duration: HIP events recorded by libpdd around the
-    # k_sweep_il launch on the stream it runs on (torch's current stream),
-    # in separate untimed steps so the timed loop above has no host syncs
-    sw.set_timing(True)
-    ks = []
-    for i in range(min(args.steps, 5)):
-        step()
-        ks.append(sw.kernel_ms())
-    sw.set_timing(False)
-    kern_ms = float(np.mean(ks))
+    kern_ms, launches = sw.timing_read() if sw is not None else (0.0, 0)
+    if sw is not None:
+        sw.set_timing(False)
     e2e = None
-    if args.e2e and args.mode == "timeblock":
+    if args.e2e and mode == "timeblock":
         # PCIe-inclusive: the boundary handed host buffers
         hx = torch.empty(x.shape, dtype=x.dtype, pin_memory=True)
         hx.copy_(x)
@@ -291,72 +351,98 @@ def main():
             hp.copy_(plane, non_blocking=True)
             torch.cuda.synchronize()
             ms.append((time.perf_counter() - t1) * 1e3)
-        e2e = {"ms_per_step": min(ms), "value": len(dms) * n_out * C / (min(ms) * 1e-3),
+        e2e = {"ms_per_step": min(ms), "value": D * n_out * C / (min(ms) * 1e-3),
                "bytes_h2d": x.numel() * x.element_size(), "bytes_d2h": plane.numel() * 4,
                "note": "best of 3; value = samples*channels*DM/s including the transfers"}
         del hx, hp, xd
+    rccl_world = dist.get_world_size() if world > 1 else 1
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-
-    units_rank = len(dms) * n_out * C           # samples*channels*DM per step on this rank
-    units_all = (D * n_out * C) * (world if args.mode == "timeblock" else 1)
-    value = units_all * args.steps / el
-    s_in = 1 if args.dtype == "u8" else 4
-    adds_per_launch = units_rank                 # one FP32 add per work unit
-    achieved_tf = adds_per_launch / (kern_ms * 1e-3) / 1e12
+    adds_rank_step = rows * n_out * C            # one add per samp*ch*DM on this rank
+    units_all = D * n_out * C * (world if mode == "timeblock" else 1)
+    value = units_all * steps / el
+    s_in = 1 if dtype == "u8" else 4
+    achieved = adds_rank_step * steps / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else None
     # LDS roof: ds_read_b128 at 256 B/clk/CU feeds 4 f32 samples (f32 path)
-    # or 8 u16 samples (8-bit path) per 16 B -> T adds/s
-    lds_roof = 256 * 2.4e9 * 16 * (8 if args.dtype == "u8" else 4) / 1e12  # CUs x clk x reads/clk
-    uniq_bytes = C * N * s_in + len(dms) * n_out * 4
-    achieved_gbs = uniq_bytes / (kern_ms * 1e-3) / 1e9
-    pmc_key = "%s_%s" % (args.config, args.dtype)
+    # or 8 u16 samples (8-bit path) per 16 B
+    lds_roof = N_CU * CLK_GHZ * 1e9 * 256 / 16 * (8 if dtype == "u8" else 4) / 1e12
+    uniq_bytes = C * N * s_in + rows * n_out * 4
+    k_s = kern_ms * 1e-3 / steps if kern_ms > 0 else None
+    pmc_key = "%s_%s" % (args.config, dtype)
     pmc = load_pmc(os.path.join(ROOT, "profiles", "pmc_sweep.json"), pmc_key)
     traffic = pmc.get("hbm_bytes_per_launch") if isinstance(pmc, dict) else None
 
     if rank == 0:
+        plan = sw.info(1 if dtype == "u8" else 0) if sw is not None else None
         line = {
             "metric": "DM-trial samples*channels/sec (node) + % HBM roofline",
             "value": value,
             "unit": "samples*channels*DM/s",
             "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": el / args.steps * 1e3,
+            "steps": steps,
+            "warmup": warmup,
+            "ms_per_step": el / steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak" if args.mode == "timeblock" else "strong",
+            "scaling": "weak" if mode == "timeblock" else "strong",
             "vs_baseline": None,
-            "dtype": args.dtype,
+            "dtype": dtype,
             "data": "synthetic (uint8 clip(round(N(128,16))) filterbank%s, generated on device)"
-                    % ("" if args.dtype == "u8" else " as float32"),
-            "config": {"workload": "brute-force DM sweep %d ch x 2^%d samples x %d DM (%g-%g pc/cc), "
-                                   "64 us, 1250-1550 MHz, trim=True" % (C, int(np.log2(N)), D,
-                                                                      cfg["dm_lo"], cfg["dm_hi"]),
+                    % ("" if dtype == "u8" else " as float32"),
+            "config": {"workload": "%s: brute-force DM sweep %d ch x 2^%d samples x %d DM "
+                                   "(%g-%g pc/cc), 64 us, 1250-1550 MHz, trim=True%s"
+                                   % ("BASELINE configs[%d]" % cfg["baseline_index"]
+                                      if cfg["baseline_index"] is not None else args.config,
+                                      C, int(np.log2(N)), D, cfg["dm_lo"], cfg["dm_hi"],
+                                      ", DM-sharded (RCCL all-gather of per-rank time-batch "
+                                      "slices, %d batch(es), planes %s)"
+                                      % (nb, "gathered to rank 0" if args.gather else
+                                         "resident per rank") if mode == "dmshard" else
+                                      ", every rank its own block"),
                        "config_name": args.config, "channels": C, "samples": N, "dm_trials": D,
-                       "n_out": n_out, "parallelism": "%s%d" % ("tb" if args.mode == "timeblock"
+                       "n_out": n_out, "parallelism": "%s%d" % ("tb" if mode == "timeblock"
                                                                 else "dm", world),
-                       "plan": sw.info(1 if args.dtype == "u8" else 0)},
-            "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_F32_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved_tf / PEAK_F32_TFLOPS,
+                       "rccl_world_size": rccl_world, "plan": plan},
+            "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_ADD_T,
+                         "unit": "T adds/s", "frac": achieved / PEAK_ADD_T if achieved else None,
                          "traffic": traffic,
-                         "kernel": "pdd::k_sweep_il", "kernel_ms": kern_ms,
-                         "note": "compute roof: one FP32 add per samp*ch*DM; no MFMA-shaped "
-                                 "work exists, the FP32 vector peak equals the FP32 dense MFMA "
-                                 "peak (157.3 TF) on gfx950; see DESIGN.md",
-                         # the roofs that actually bind an add-only, LDS-fed kernel
-                         "add_peak": PEAK_ADD_T, "frac_add_peak": achieved_tf / PEAK_ADD_T,
-                         "lds_roof": lds_roof, "frac_lds_roof": achieved_tf / lds_roof},
-            "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": PEAK_HBM_GBS,
-                             "unit": "GB/s", "frac": achieved_gbs / PEAK_HBM_GBS,
-                             "bytes_per_launch": uniq_bytes},
+                         "traffic_source": ("profiles/pmc_sweep.json[%s] (separate rocprofv3 "
+                                            "--pmc FETCH_SIZE / WRITE_SIZE passes of this "
+                                            "command)" % pmc_key) if traffic else None,
+                         "kernel": "pdd::k_sweep_il", "kernel_ms_per_launch":
+                             kern_ms / launches if launches else None,
+                         "launches_per_step": launches / steps if launches else None,
+                         "kernel_s_per_step": k_s,
+                         "adds_per_step_rank0": adds_rank_step,
+                         "note": "the sweep does one FP32/integer add per samp*ch*DM and no "
+                                 "MFMA-shaped work; its binding roof is the VALU add rate "
+                                 "(v_pk_add_f32 / two u16 lanes per v_add_u32), with the LDS "
+                                 "read roof beside it (DESIGN.md §3-4)",
+                         "lds_roof": lds_roof,
+                         "frac_lds_roof": achieved / lds_roof if achieved else None},
+            "roofline_hbm": {"bound": "hbm", "achieved": uniq_bytes / k_s / 1e9 if k_s else None,
+                             "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": uniq_bytes / k_s / 1e9 / PEAK_HBM_GBS if k_s else None,
+                             "bytes_per_step": uniq_bytes,
+                             "note": "unique bytes (input once + plane once) over the sweep "
+                                     "kernel time: capped at a few % for a sweep (SURVEY.md "
+                                     "§8(d))"},
             "cpu_baseline": None,
         }
         if e2e is not None:
             line["end_to_end_pcie"] = e2e
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_trials, dt)
-        print(json.dumps(line))
+            del step
+            if mode == "dmshard":
+                del part
+            else:
+                del x
+            torch.cuda.empty_cache()
+            cC, cn, ct = cfg["cpu"]
+            log("cpu baseline: %d ch x %d samples, %d trials" % (cC, cn, ct))
+            line["cpu_baseline"] = cpu_baseline(cC, cn, dms_all, args.cpu_trials or ct, dt, N)
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -627,11 +713,11 @@ def stream_bench(args, cfg, rank, world, dev):
                    "downsamp": ds, "dm_trials": D, "parallelism": "tb%d" % world},
         "realtime_factor": (block * dt) / (ms * 1e-3),
         "input_spectra_per_s": in_rate,
-        "roofline": {"bound": "mfma", "achieved": D * nb * C / (ms * 1e-3) / 1e12,
-                     "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
-                     "frac": D * nb * C / (ms * 1e-3) / 1e12 / PEAK_F32_TFLOPS, "traffic": None,
-                     "note": "whole-step time (H2D, prologue, sweep) per block; one FP32 add "
-                             "per unit"},
+        "roofline": {"bound": "valu", "achieved": D * nb * C / (ms * 1e-3) / 1e12,
+                     "peak": PEAK_ADD_T, "unit": "T adds/s",
+                     "frac": D * nb * C / (ms * 1e-3) / 1e12 / PEAK_ADD_T, "traffic": None,
+                     "note": "whole-step time (H2D, prologue, sweep) per block; one add per "
+                             "unit against the VALU add roof"},
         "cpu_baseline": None,
     }
     st.close()
@@ -643,12 +729,12 @@ def subband_bench(args, cfg, rank, world, dev):
     grid (Observation(64us, 1400, 300, 4096).gen_ddplan(0, 1000, 64, 0.5)):
     per DDstep downsample, then all 40 subband passes as ONE grouped sweep
     (stage 1) and all passes' DM sweeps as ONE grouped sweep (stage 2)
-    (pypulsar_amd.sweep.execute_plan_grouped; equal to the per-pass
+    (pypulsar_amd.sweep.DDplanExecutor, plans built once; equal to the per-pass
     subband(64, subDM) + sweep executor, tests/test_gpu_grouped.py).  Work
     units are the equivalent brute-force samples*channels*DM of the plan's
     trials (the quantity the two-stage method replaces)."""
     from pypulsar_amd.formats.spectra import Spectra
-    from pypulsar_amd.sweep import execute_plan_grouped
+    from pypulsar_amd.sweep import DDplanExecutor
     from pypulsar_amd.utils.ddplan import Observation
     C, N = cfg["C"], cfg["N"]
     dt = 64e-6
@@ -664,8 +750,11 @@ def subband_bench(args, cfg, rank, world, dev):
         mb = int(max(0, sweep_table(step.DMs[-1:], freqs, dt * step.downsamp).max()))
         units += len(step.DMs) * (n_ds - mb) * C
 
+    # delay tables, grouped plans and buffers built once per grid
+    ex = DDplanExecutor(plan, freqs, dt, N, raw8=True)
+
     def one():
-        return execute_plan_grouped(s, plan, padval=0)
+        return ex(s, padval=0)
 
     for _ in range(args.warmup):
         one()

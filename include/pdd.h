@@ -167,11 +167,15 @@ int pdd_sweep_execute_grouped(const pdd_sweep_plan* plan, const void* x, int64_t
  * DMs per block, time samples per block, LDS bytes per workgroup. */
 int pdd_sweep_plan_info(const pdd_sweep_plan* plan, int64_t* info /*[8]*/);
 int pdd_sweep_plan_destroy(pdd_sweep_plan* plan);
-/* Measurement hooks (bench.py): with timing on, pdd_sweep_execute brackets
- * the sweep kernel(s) -- not the interleave pre-pass -- with HIP events on
- * the execute stream; pdd_sweep_kernel_ms waits for and returns the last
- * bracketed duration. */
+/* Measurement hooks (bench.py): with timing on, every sweep-kernel launch
+ * of pdd_sweep_execute(_grouped) -- not the interleave pre-pass -- is
+ * bracketed by its own pair of HIP events on the execute stream (no host
+ * synchronisation; up to 1024 launches between reads).
+ * pdd_sweep_timing_read waits for the last one and returns the SUM of the
+ * bracketed durations and the number of launches since the previous read;
+ * pdd_sweep_kernel_ms is the same sum alone. */
 int pdd_sweep_set_timing(pdd_sweep_plan* plan, int on);
+int pdd_sweep_timing_read(pdd_sweep_plan* plan, float* total_ms, int64_t* launches);
 int pdd_sweep_kernel_ms(pdd_sweep_plan* plan, float* ms);
 
 /* ---- single-pulse boxcar search over a DM-time plane (SURVEY.md §8(f)

@@ -214,6 +214,26 @@ def sweep_plane(data, table, padval=0, n_out=None):
     return np.array([shifted_sum(data, table[d], padval)[:n_out] for d in range(table.shape[0])])
 
 
+def sweep_rows_inside(data, table, n_out):
+    """sweep_plane rows for trials whose reads t + table[d, c], t < n_out, all
+    fall inside [0, N) (no pad is read; the trim=True rows of a grid with
+    delays >= 0): the same sums as shifted_sum, taken as channel slices with
+    exact int64 accumulation for integer data -- fast enough for 4096-channel
+    rows at full length."""
+    data = np.asarray(data)
+    C, N = data.shape
+    table = np.atleast_2d(np.asarray(table))
+    integer = np.issubdtype(data.dtype, np.integer)
+    out = np.zeros((table.shape[0], n_out), dtype=np.int64 if integer else np.float64)
+    for d in range(table.shape[0]):
+        acc = out[d]
+        for c in range(C):
+            b = int(table[d, c])
+            assert 0 <= b and b + n_out <= N, "row %d reads a pad (bin %d)" % (d, b)
+            acc += data[c, b:b + n_out]
+    return out.astype(np.float64)
+
+
 # --------------------------------------------------------------------------
 # waterfaller post-chain (formats/spectra.py:140-227, 262-303)
 # --------------------------------------------------------------------------

@@ -28,7 +28,7 @@ EXPORTS = (
     "pdd_sweep_plan_destroy", "pdd_global_stats", "pdd_scale_rows", "pdd_masked_fill",
     "pdd_smooth", "pdd_zdm_downsample", "pdd_sweep_set_timing", "pdd_sweep_kernel_ms",
     "pdd_sweep_plan_create_grouped", "pdd_sweep_execute_grouped", "pdd_sp_chunk_stats",
-    "pdd_sp_search", "pdd_psrfits_subints", "pdd_downsample_u8",
+    "pdd_sp_search", "pdd_psrfits_subints", "pdd_downsample_u8", "pdd_sweep_timing_read",
 )
 
 
@@ -70,6 +70,7 @@ _SIGS = {
     "pdd_sweep_execute_grouped": ([_vp, _vp, _i64, _i64, _int, _vp, _vp, _i64, _i64, _i64, _i64,
                                    _vp], _int),
     "pdd_sweep_kernel_ms": ([_vp, ctypes.POINTER(ctypes.c_float)], _int),
+    "pdd_sweep_timing_read": ([_vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(_i64)], _int),
     "pdd_sp_chunk_stats": ([_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp], _int),
     "pdd_sp_search": ([_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i64,
                        _vp, _int, ctypes.c_float, _vp, _i64, _vp, _vp], _int),

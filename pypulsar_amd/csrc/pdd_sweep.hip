@@ -1830,9 +1830,13 @@ struct pdd_sweep_plan {
   int P = 0;               // ring kernel: prefetch distance (channels)
   int dtype = PDD_F32;     // input element type
   int64_t n_grp = 1;       // independent channel groups (grouped sweep)
-  hipEvent_t ev[2] = {nullptr, nullptr};  // timing of the sweep kernel (pdd_sweep_set_timing)
+  // timing of the sweep kernel (pdd_sweep_set_timing): one event pair per
+  // bracketed launch, recorded on the execute stream without host syncs
+  static constexpr int kEvPairs = 1024;
+  hipEvent_t* ev = nullptr;  // [2 * kEvPairs]
   int timing = 0;
-  int timed = 0;           // launches bracketed since the last query
+  int timed = 0;             // launches bracketed since the last query
+  int dropped = 0;           // launches past the pool (not bracketed)
 };
 
 using namespace pdd;
@@ -1855,7 +1859,10 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
   int64_t seg = (nr_max - (hi - lo) - 64) / Tq * Tq * SP;  // output samples per segment
   PDD_REQUIRE(seg > 0, "pdd_sweep_execute: delay span %lld too wide for the segment budget",
               (long long)(hi - lo));
-  seg = std::min(seg, cdiv(n_out, (int64_t)SP * Tq) * SP * Tq);
+  // equal segments (whole tiles): every launch does the same work
+  const int64_t tile_s = (int64_t)SP * Tq;
+  const int64_t nseg = cdiv(n_out, seg);
+  seg = cdiv(cdiv(n_out, nseg), tile_s) * tile_s;
   const int64_t qs_max = seg / SP;
   const int64_t nr_alloc = qs_max + (hi - lo) + 64;
   float4* R = nullptr;
@@ -1881,16 +1888,19 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
     const int64_t n_tblk = Qs / Tq;
     const int64_t blocks = n_tblk * p->n_dblk * p->n_grp;
     if (blocks >= (1ll << 31)) { rc = -1; break; }
-    if (p->timing && t_base == 0) (void)hipEventRecord(p->ev[0], st);
+    pdd_sweep_plan* pm = const_cast<pdd_sweep_plan*>(p);
+    const bool bracket = p->timing && p->timed < pdd_sweep_plan::kEvPairs;
+    if (p->timing && !bracket) pm->dropped++;
+    if (bracket) (void)hipEventRecord(p->ev[2 * p->timed], st);
     hipLaunchKernelGGL(il_kernel_for(p->v), dim3((unsigned)blocks), dim3(p->v.threads()),
                        p->lds_bytes, st, R, nR, (int)p->C, (int)lo, p->d_tab, out, ld_out,
                        (int)p->D, Qs, t_base, t_base + cnt, p->stride, (int)n_tblk,
                        (int)p->n_dblk, dbg, row_g, row_d);
     if (hipGetLastError() != hipSuccess) rc = -3;
-  }
-  if (p->timing) {
-    (void)hipEventRecord(p->ev[1], st);
-    const_cast<pdd_sweep_plan*>(p)->timed = 1;
+    if (bracket) {
+      (void)hipEventRecord(p->ev[2 * p->timed + 1], st);
+      pm->timed++;
+    }
   }
   (void)hipFreeAsync(R, st);
   if (rc == -1) set_error("pdd_sweep_execute: grid too large");
@@ -2135,28 +2145,46 @@ int pdd_sweep_execute_grouped(const pdd_sweep_plan* p, const void* x, int64_t N,
 
 int pdd_sweep_set_timing(pdd_sweep_plan* p, int on) {
   PDD_REQUIRE(p, "pdd_sweep_set_timing: null pointer");
-  if (on && !p->ev[0]) {
-    PDD_HIP(hipEventCreate(&p->ev[0]));
-    PDD_HIP(hipEventCreate(&p->ev[1]));
+  if (on && !p->ev) {
+    p->ev = new hipEvent_t[2 * pdd_sweep_plan::kEvPairs]();
+    for (int i = 0; i < 2 * pdd_sweep_plan::kEvPairs; ++i) PDD_HIP(hipEventCreate(&p->ev[i]));
   }
   p->timing = on ? 1 : 0;
+  p->timed = 0;
+  p->dropped = 0;
+  return 0;
+}
+
+int pdd_sweep_timing_read(pdd_sweep_plan* p, float* total_ms, int64_t* launches) {
+  PDD_REQUIRE(p && total_ms && launches, "pdd_sweep_timing_read: null pointer");
+  PDD_REQUIRE(p->timing && p->timed, "pdd_sweep_timing_read: no timed launch (pdd_sweep_set_timing)");
+  PDD_REQUIRE(!p->dropped, "pdd_sweep_timing_read: %d launches past the %d-pair event pool",
+              p->dropped, pdd_sweep_plan::kEvPairs);
+  PDD_HIP(hipEventSynchronize(p->ev[2 * p->timed - 1]));
+  double sum = 0.0;
+  for (int i = 0; i < p->timed; ++i) {
+    float ms = 0.f;
+    PDD_HIP(hipEventElapsedTime(&ms, p->ev[2 * i], p->ev[2 * i + 1]));
+    sum += ms;
+  }
+  *total_ms = (float)sum;
+  *launches = p->timed;
   p->timed = 0;
   return 0;
 }
 
 int pdd_sweep_kernel_ms(pdd_sweep_plan* p, float* ms) {
-  PDD_REQUIRE(p && ms, "pdd_sweep_kernel_ms: null pointer");
-  PDD_REQUIRE(p->timing && p->timed, "pdd_sweep_kernel_ms: no timed launch (pdd_sweep_set_timing)");
-  PDD_HIP(hipEventSynchronize(p->ev[1]));
-  PDD_HIP(hipEventElapsedTime(ms, p->ev[0], p->ev[1]));
-  p->timed = 0;
-  return 0;
+  int64_t n = 0;
+  return pdd_sweep_timing_read(p, ms, &n);
 }
 
 int pdd_sweep_plan_destroy(pdd_sweep_plan* p) {
   if (!p) return 0;
-  if (p->ev[0]) (void)hipEventDestroy(p->ev[0]);
-  if (p->ev[1]) (void)hipEventDestroy(p->ev[1]);
+  if (p->ev) {
+    for (int i = 0; i < 2 * pdd_sweep_plan::kEvPairs; ++i)
+      if (p->ev[i]) (void)hipEventDestroy(p->ev[i]);
+    delete[] p->ev;
+  }
   if (p->d_tab) (void)hipFree(p->d_tab);
   if (p->d_bmin) (void)hipFree(p->d_bmin);
   if (p->d_bspan) (void)hipFree(p->d_bspan);

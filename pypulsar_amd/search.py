@@ -28,6 +28,7 @@ from ._lib import call, ptr, stream_ptr
 
 DEFAULT_WIDTHS = (1, 2, 3, 4, 6, 9, 14, 20, 30, 45, 70, 100, 150)
 WINDOW = 1024  # starts per candidate window (kSpWin in pdd_search.hip)
+PREFIX_BLOCK = 4096  # starts per k_sp_search block: its prefix sums restart there (kSpStarts)
 
 CAND_DTYPE = np.dtype([("DM", "f8"), ("Sigma", "f4"), ("Time", "f8"), ("Sample", "i8"),
                        ("Downfact", "i4"), ("row", "i4")])
@@ -122,9 +123,12 @@ class StreamingSearch(object):
     block's rows continued into the next block's plane, so the candidates
     equal those of a one-shot search of the whole stream's plane.  Needs the
     plane block width (block / downsamp) to be a multiple of the detrend
-    length and of the 1024-start window.  Yields candidate record arrays.
-    Preallocated ``planes`` (see StreamingSweep) must number at least 2: a
-    block's plane is read again when the next block's plane is searched."""
+    length and of the 4096-start search block (k_sp_search's prefix sums
+    restart every 4096 starts, so equal S/N bits -- hence equal candidates --
+    need the stream's block seams on those boundaries).  Yields candidate
+    record arrays.  Preallocated ``planes`` (see StreamingSweep) must number
+    at least 2: a block's plane is read again when the next block's plane is
+    searched (they rotate by emitted block, so 2 suffice)."""
 
     def __init__(self, dms, freqs, dt, block=1 << 18, downsamp=2, zero_dm=True, dtype=None,
                  threshold=6.0, widths=DEFAULT_WIDTHS, detrendlen=1024, max_cands=1 << 20):
@@ -134,8 +138,8 @@ class StreamingSearch(object):
                                     zero_dm=zero_dm, **kw)
         self.search = SinglePulseSearch(threshold, widths, detrendlen, max_cands)
         nb = self.sweep.n_out_block
-        assert nb % detrendlen == 0 and nb % WINDOW == 0, \
-            "block/downsamp must be a multiple of detrendlen and of %d" % WINDOW
+        assert nb % detrendlen == 0 and nb % PREFIX_BLOCK == 0, \
+            "block/downsamp must be a multiple of detrendlen and of %d" % PREFIX_BLOCK
         self.dms = np.asarray(dms, dtype=np.float64)
         self.dt = dt * downsamp
 

@@ -2,19 +2,24 @@
 
 Two partitions:
 
-* **DM sharding** (one block, many GPUs): rank ``src`` holds the filterbank
-  block; it is broadcast to every rank over RCCL (xGMI), each rank sweeps a
-  contiguous slice of the DM grid balanced by work (``dm_slices``), and the
-  DM-time planes are gathered to ``dst``.  The collectives are the real
-  exchange steps of this partition: the block in, the planes out.
+* **DM sharding** (one block, many GPUs; the north star and BASELINE
+  configs[3]): every GPU needs the whole filterbank block and owns a
+  contiguous slice of the DM grid, balanced by DDplan work fraction
+  (``dm_slices``; DDplan2b.py:272-273).  ``DMShardedSweep`` is the pipelined
+  production path: the block enters as per-rank H2D slices assembled by RCCL
+  all-gathers over xGMI, one time batch at a time, and batch k+1's all-gather
+  runs on the communicator's stream while batch k is corner-turned and swept;
+  planes stay resident on their rank (or, with ``gather=True``, each batch's
+  rows are sent to ``dst`` while the next batch is swept).  The collectives
+  are the real exchange steps of this partition: the block in, the planes out.
 * **time-block sharding** (independent blocks): rank r sweeps its own range of
   output samples, reading input ``[a, b + max_bin)`` (the overlap equals the
   largest delay), with no collective at all; concatenating the ranks' planes
-  equals the one-shot plane.  This is what ``bench.py`` runs by default.
+  equals the one-shot plane.
 
 The backend is whatever the process group was initialised with: "nccl"
-(RCCL) on the GPU box, "gloo" in the CPU tests, where ``sweep_fn`` is
-injected by the test.
+(RCCL) on the GPU box, "gloo" in the CPU tests, where the per-rank compute
+(``to_cm``, ``sweep_fn``) is injected by the test.
 """
 import numpy as np
 import torch
@@ -36,6 +41,21 @@ def dm_slices(D, world, work=None):
     return [(int(bounds[r]), int(bounds[r + 1])) for r in range(world)]
 
 
+def trial_work(dms, downsamp=1):
+    """Per-trial work weights of a DM grid: DDplan2b's work fraction is
+    numDMs/downsamp per step (DDplan2b.py:272-273), i.e. 1/downsamp per
+    trial.  ``downsamp`` may be a scalar or one value per trial."""
+    d = np.broadcast_to(np.asarray(downsamp, dtype=np.float64), (len(dms),))
+    return 1.0 / d
+
+
+def plan_trial_work(ddplan):
+    """(dms, work) over all steps of a DDplan (concatenated in step order)."""
+    dms = np.concatenate([np.asarray(s.DMs, dtype=np.float64) for s in ddplan.DDsteps])
+    work = np.concatenate([trial_work(s.DMs, s.downsamp) for s in ddplan.DDsteps])
+    return dms, work
+
+
 def timeblock_ranges(n_out, world, max_bin):
     """Per rank: (out_lo, out_hi, in_lo, in_hi) so rank r computes plane
     columns [out_lo, out_hi) from input samples [in_lo, in_hi) with
@@ -54,6 +74,15 @@ def broadcast_block(x, src=0, group=None):
     return x
 
 
+def _all_gather_into(out, part, group=None, async_op=False):
+    """out[r*n:(r+1)*n] = rank r's ``part`` (RCCL all-gather on the GPU box;
+    per-rank views on gloo)."""
+    world = dist.get_world_size(group)
+    if part.is_cuda and hasattr(dist, "all_gather_into_tensor"):
+        return dist.all_gather_into_tensor(out, part, group=group, async_op=async_op)
+    return dist.all_gather(list(out.chunk(world)), part, group=group, async_op=async_op)
+
+
 def allgather_block(part, group=None):
     """Assemble a time-major block from per-rank slices: rank r holds spectra
     [r*n, (r+1)*n) ([n, C], e.g. its own H2D of 1/world of the pinned host
@@ -65,70 +94,238 @@ def allgather_block(part, group=None):
     world = dist.get_world_size(group)
     out = torch.empty((part.shape[0] * world,) + tuple(part.shape[1:]), dtype=part.dtype,
                       device=part.device)
-    if hasattr(dist, "all_gather_into_tensor") and part.is_cuda:
-        dist.all_gather_into_tensor(out, part.contiguous(), group=group)
-    else:
-        dist.all_gather(list(out.chunk(world)), part.contiguous(), group=group)
+    _all_gather_into(out, part.contiguous(), group=group)
     return out
 
 
-def dm_sharded_sweep_ag(part_tc, dms, freqs, dt, n_out, sweep_fn=None, to_cm=None, work=None,
-                        group=None):
-    """DM sharding with the all-gather input exchange: every rank contributes
-    its slice of the time-major block, all ranks assemble it
-    (``allgather_block``), corner-turn it to [C, N] (``to_cm``, default
-    pdd_corner_turn) and sweep their own DM slice; the plane stays on the
-    rank (returned with the slice) for a downstream search."""
+def _codes():
+    from . import _lib
+    return {torch.uint8: _lib.U8, torch.float32: _lib.F32}
+
+
+def _corner_turn(src_tc, dst_cm):
+    """pdd_corner_turn of a time-major [n, C] block into the channel-major
+    [C, n] view ``dst_cm`` (row stride = the full block's length)."""
+    from ._lib import call, ptr, stream_ptr
+    n, C = src_tc.shape
+    code = _codes()[src_tc.dtype]
+    call("pdd_corner_turn", ptr(src_tc), code, n, C, src_tc.stride(0), ptr(dst_cm), code,
+         dst_cm.stride(0), stream_ptr())
+
+
+class DMShardedSweep(object):
+    """Pipelined DM-sharded sweep of ONE filterbank block across the ranks
+    (north star; BASELINE configs[3]).
+
+    Semantics: rank r produces rows [lo_r, hi_r) of the one-shot plane
+    ``plane[d][t] = sum_c X(c, t + bins[d][c])``, t < n_out = N - max bin of
+    the WHOLE grid (per DM trial: Spectra.dedisperse(dms[d], trim=True) +
+    channel sum, formats/spectra.py:229-260 + bin/waterfaller.py:140),
+    delivered as ``n_batches`` column blocks ``planes[k]`` ([rows, cols_k],
+    columns [col_edges[k], col_edges[k+1])).
+
+    Input layout (file order, time-major): the block is cut into ``n_batches``
+    time batches of T = N / n_batches spectra; rank r holds, for each batch k,
+    spectra [k*T + r*T/W, k*T + (r+1)*T/W) -- ``part`` is [n_batches, T/W, C]
+    (its own 1/W H2D slice of every batch).
+
+    One ``__call__`` (a bench step):
+        issue all-gather of batch 0
+        for k in 0..n_batches-1:
+            wait batch k; issue all-gather of batch k+1  (overlaps the sweep below)
+            corner-turn batch k -> x[:, kT:(k+1)T]        (pdd_corner_turn)
+            sweep plane columns [col_edges[k], col_edges[k+1]) of this rank's
+              DM slice from x[:, col_edges[k] : col_edges[k+1] + max_bin]
+            (gather=True: send this batch's rows to ``dst``, async, which
+             receives them into its full [D, cols_k] batch plane)
+    Column block k needs input up to col_edges[k+1] + max_bin <= (k+1)T, so it
+    is computable as soon as batch k has arrived.  All delays are >= 0 here
+    (cur_dm = 0, dms >= 0, reference = the highest frequency), so no pad value
+    is ever read and a view of x is exactly the reference's input.
+
+    Plans (delay table, sweep plan, buffers) are built once in __init__;
+    ``work`` (per-trial weights, e.g. ``trial_work``) balances the DM slices.
+    ``to_cm(src_tc, dst_cm_view)`` and ``sweep_fn(x_view, dms_slice, out, n_cols)`` are
+    injected by the CPU tests; the defaults are pdd_corner_turn and the HIP
+    DMSweep of this rank's slice (built once).
+    """
+
+    def __init__(self, dms, freqs, dt, N, dtype=torch.uint8, n_batches=1, work=None,
+                 gather=False, dst=0, group=None, device=None, to_cm=None, sweep_fn=None):
+        from . import delays as _delays
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.dms = np.asarray(dms, dtype=np.float64)
+        self.freqs = np.asarray(freqs, dtype=np.float64)
+        self.C = len(self.freqs)
+        self.N = int(N)
+        self.D = len(self.dms)
+        self.dt = dt
+        self.dtype = dtype
+        self.device = torch.device("cpu") if device is None else torch.device(device)
+        self.nb = int(n_batches)
+        assert self.N % (self.nb * self.world) == 0, \
+            "N must split into n_batches x world equal slices"
+        self.T = self.N // self.nb
+        tab = _delays.sweep_table(self.dms, self.freqs, dt)
+        assert tab.size == 0 or tab.min() >= 0, "DM-sharded sweep expects delays >= 0"
+        self.max_bin = int(tab.max()) if tab.size else 0
+        self.n_out = self.N - self.max_bin
+        assert self.n_out > 0 and self.T > self.max_bin, \
+            "each time batch must be longer than the largest delay"
+        edges = [0]
+        for k in range(self.nb):
+            edges.append(min(self.n_out, (k + 1) * self.T - self.max_bin))
+        edges[-1] = self.n_out
+        self.col_edges = edges
+        self.slices = dm_slices(self.D, self.world, work)
+        self.lo, self.hi = self.slices[self.rank]
+        self.rows = self.hi - self.lo
+        self.gather = bool(gather)
+        self.dst = dst
+        # buffers (reused every call); one rank corner-turns its part directly
+        self.xt = (torch.empty((self.N, self.C), dtype=dtype, device=self.device)
+                   if self.world > 1 else None)                                    # time-major
+        self.x = torch.empty((self.C, self.N), dtype=dtype, device=self.device)   # channel-major
+        cols = [edges[k + 1] - edges[k] for k in range(self.nb)]
+        if self.gather and self.rank == self.dst:
+            # dst's full batch planes; its own rows are views of them
+            self.full = [torch.empty((self.D, c), dtype=torch.float32, device=self.device)
+                         for c in cols]
+            self.planes = [f[self.lo:self.hi] for f in self.full]
+        else:
+            self.full = None
+            self.planes = [torch.empty((self.rows, c), dtype=torch.float32, device=self.device)
+                           for c in cols]
+        self.to_cm = to_cm if to_cm is not None else _corner_turn
+        self.sw = None
+        if sweep_fn is None:
+            from .sweep import DMSweep
+            code = "u8" if dtype == torch.uint8 else "f32"
+            if self.rows:
+                self.sw = DMSweep(self.dms[self.lo:self.hi], self.freqs, dt, dtype=code)
+
+            def sweep_fn(xv, dms_slice, out, n_cols):
+                self.sw(xv, out=out, n_out=n_cols)
+        self.sweep_fn = sweep_fn
+
+    def __call__(self, part):
+        """Run one pipelined sweep of the block whose per-rank slices are
+        ``part`` ([n_batches, T/W, C]).  Returns this rank's batch planes
+        (with ``gather``: the full [D, cols_k] batch planes on ``dst``)."""
+        nb, W = self.nb, self.world
+        assert tuple(part.shape) == (nb, self.T // W, self.C) and part.dtype == self.dtype
+        T = self.T
+
+        def issue(k):
+            if W == 1:
+                return None
+            return _all_gather_into(self.xt[k * T:(k + 1) * T], part[k], group=self.group,
+                                    async_op=True)
+
+        sends = []
+        pending = issue(0)
+        for k in range(nb):
+            if pending is not None:
+                pending.wait()
+            pending = issue(k + 1) if k + 1 < nb else None
+            rows = part[k] if W == 1 else self.xt[k * T:(k + 1) * T]
+            self.to_cm(rows, self.x[:, k * T:(k + 1) * T])
+            a, b = self.col_edges[k], self.col_edges[k + 1]
+            if self.rows and b > a:
+                self.sweep_fn(self.x[:, a:b + self.max_bin], self.dms[self.lo:self.hi],
+                              self.planes[k], b - a)
+            if self.gather:
+                sends += self._gather_batch(k)
+        for w in sends:
+            w.wait()
+        return self.full if (self.gather and self.rank == self.dst) else self.planes
+
+    def _gather_batch(self, k):
+        """Rows of batch k to ``dst`` (point-to-point, async): dst receives each
+        rank's rows straight into its full batch plane (contiguous row range),
+        no concatenation."""
+        if self.world == 1:
+            return []
+        if self.rank != self.dst:
+            return [dist.isend(self.planes[k], self.dst, group=self.group)] if self.rows else []
+        works = []
+        for r, (lo, hi) in enumerate(self.slices):
+            if r != self.dst and hi > lo:
+                works.append(dist.irecv(self.full[k][lo:hi], r, group=self.group))
+        return works
+
+    def plane(self):
+        """This rank's rows (or dst's full plane with ``gather``) as one
+        [rows, n_out] tensor (a copy; for tests and downstream consumers that
+        want a single plane -- not used in the timed path)."""
+        src = self.full if (self.gather and self.rank == self.dst) else self.planes
+        return torch.cat(list(src), dim=1)
+
+    def close(self):
+        if self.sw is not None:
+            self.sw.close()
+            self.sw = None
+
+
+def split_block(block_tc, n_batches, world, rank):
+    """This rank's ``part`` of a time-major [N, C] block for DMShardedSweep:
+    [n_batches, N/(n_batches*world), C] (a copy)."""
+    N, C = block_tc.shape
+    T = N // n_batches
+    n = T // world
+    v = block_tc.reshape(n_batches, world, n, C)
+    return v[:, rank].contiguous()
+
+
+def gather_planes(plane, slices, dst=0, group=None, out=None):
+    """Gather per-rank planes (rows = that rank's DM slice) to ``dst`` into
+    the preallocated [D, n_out] ``out`` (allocated if None): dst receives each
+    rank's rows straight into its row range (point-to-point), no padding and
+    no concatenation.  Returns ``out`` on dst, None elsewhere."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    slices = dm_slices(len(dms), world, work)
-    blk = allgather_block(part_tc, group=group)
-    if to_cm is None:
-        from ._lib import call, ptr, stream_ptr
-        from . import _lib
-        codes = {torch.uint8: _lib.U8, torch.float32: _lib.F32}
-        N, C = blk.shape
-        x = torch.empty((C, N), dtype=blk.dtype, device=blk.device)
-        call("pdd_corner_turn", ptr(blk), codes[blk.dtype], N, C, C, ptr(x), codes[blk.dtype],
-             N, stream_ptr())
-    else:
-        x = to_cm(blk)
-    lo, hi = slices[rank]
-    if sweep_fn is None:
-        from .sweep import DMSweep
-
-        def sweep_fn(b, sub):
-            code = "u8" if b.dtype == torch.uint8 else "f32"
-            out = torch.empty((len(sub), n_out), dtype=torch.float32, device=b.device)
-            DMSweep(sub, freqs, dt, dtype=code)(b, out=out)
-            return out
-    part = sweep_fn(x, dms[lo:hi])[:, :n_out] if hi > lo else None
-    return (lo, hi), part
-
-
-def gather_planes(plane, slices, dst=0, group=None):
-    """Gather per-rank planes (rows = that rank's DM slice) to ``dst``;
-    returns the full [D, n_out] plane on dst, None elsewhere.  Planes are
-    padded to the largest slice so every rank sends one equal-size tensor."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    rows = max(hi - lo for lo, hi in slices)
-    n_out = plane.shape[1]
-    buf = torch.zeros((rows, n_out), dtype=plane.dtype, device=plane.device)
-    buf[: plane.shape[0]] = plane
-    gl = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
-    dist.gather(buf, gather_list=gl, dst=dst, group=group)
     if rank != dst:
+        if plane.shape[0]:
+            dist.send(plane.contiguous(), dst, group=group)
         return None
-    return torch.cat([gl[r][: hi - lo] for r, (lo, hi) in enumerate(slices)], dim=0)
+    D = slices[-1][1]
+    if out is None:
+        out = torch.empty((D, plane.shape[1]), dtype=plane.dtype, device=plane.device)
+    lo, hi = slices[dst]
+    out[lo:hi] = plane
+    works = []
+    for r in range(world):
+        lo, hi = slices[r]
+        if r != dst and hi > lo:
+            works.append(dist.irecv(out[lo:hi], r, group=group))
+    for w in works:
+        w.wait()
+    return out
+
+
+def _default_sweep_fn(freqs, dt, n_out):
+    """HIP DMSweep of a DM slice at the GLOBAL plane width ``n_out``."""
+    from .sweep import DMSweep
+
+    def fn(blk, sub):
+        code = "u8" if blk.dtype == torch.uint8 else "f32"
+        sw = DMSweep(sub, freqs, dt, dtype=code)
+        out = torch.empty((len(sub), n_out), dtype=torch.float32, device=blk.device)
+        sw(blk, out=out, n_out=n_out)
+        sw.close()
+        return out
+    return fn
 
 
 def dm_sharded_sweep(x, shape, dtype, dms, freqs, dt, n_out, sweep_fn=None, src=0, dst=0,
                      work=None, group=None, device=None):
     """Broadcast one block from ``src``, sweep this rank's DM slice, gather the
-    planes to ``dst``.  ``x`` is the block on ``src`` (ignored elsewhere).
+    planes to ``dst`` (the simple, unpipelined form of DMShardedSweep).
+    ``x`` is the [C, N] block on ``src`` (ignored elsewhere).
     ``sweep_fn(x, dms_slice) -> [len(slice), n_out] plane`` defaults to the
-    HIP DMSweep."""
+    HIP DMSweep at the global width ``n_out``."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     slices = dm_slices(len(dms), world, work)
@@ -137,14 +334,7 @@ def dm_sharded_sweep(x, shape, dtype, dms, freqs, dt, n_out, sweep_fn=None, src=
     broadcast_block(x, src=src, group=group)
     lo, hi = slices[rank]
     if sweep_fn is None:
-        from .sweep import DMSweep
-
-        def sweep_fn(blk, sub):
-            code = "u8" if blk.dtype == torch.uint8 else "f32"
-            sw = DMSweep(sub, freqs, dt, dtype=code)
-            out = torch.empty((len(sub), n_out), dtype=torch.float32, device=blk.device)
-            sw(blk, out=out)
-            return out
+        sweep_fn = _default_sweep_fn(freqs, dt, n_out)
     if hi > lo:
         part = sweep_fn(x, dms[lo:hi])[:, :n_out]
     else:
@@ -179,14 +369,7 @@ def dm_sharded_search(x, shape, dtype, dms, freqs, dt, n_out, sweep_fn=None, sea
     broadcast_block(x, src=src, group=group)
     lo, hi = slices[rank]
     if sweep_fn is None:
-        from .sweep import DMSweep
-
-        def sweep_fn(blk, sub):
-            code = "u8" if blk.dtype == torch.uint8 else "f32"
-            sw = DMSweep(sub, freqs, dt, dtype=code)
-            out = torch.empty((len(sub), n_out), dtype=torch.float32, device=blk.device)
-            sw(blk, out=out)
-            return out
+        sweep_fn = _default_sweep_fn(freqs, dt, n_out)
     if search_fn is None:
         from .search import SinglePulseSearch
         sps = SinglePulseSearch(threshold=threshold)

@@ -88,11 +88,14 @@ class StreamingSweep(object):
         """chunks: iterable of host tensors [n, C] (pinned for an asynchronous
         copy; every chunk but the last must hold exactly ``block`` spectra).
         planes: optional list of preallocated [D, block/ds] device planes,
-        used in rotation.  Yields (t0, plane)."""
+        used in rotation by EMITTED-block count (block j -> planes[j % len]),
+        so a consumer holding the last len(planes) - 1 planes never sees them
+        overwritten.  Yields (t0, plane)."""
         cur = torch.cuda.current_stream(self.device)
         prev = None  # (buffer index, n spectra)
         t0 = 0
         i = -1
+        emitted = 0
         for i, chunk in enumerate(chunks):
             b = i % self.nbuf
             n = chunk.shape[0]
@@ -113,7 +116,8 @@ class StreamingSweep(object):
                 cur.wait_event(self.h2d_head[b])   # the next chunk's first ov spectra
                 if head:
                     self.raw[pb][pn:pn + head].copy_(self.raw[b][:head])
-                out = None if planes is None else planes[pb % len(planes)]
+                out = None if planes is None else planes[emitted % len(planes)]
+                emitted += 1
                 plane = self._process(self.raw[pb], pn + head, out)
                 self.free[pb].record(cur)
                 yield t0, plane
@@ -122,7 +126,7 @@ class StreamingSweep(object):
         if prev is not None:
             pb, pn = prev
             cur.wait_event(self.h2d[pb])
-            out = None if planes is None else planes[pb % len(planes)]
+            out = None if planes is None else planes[emitted % len(planes)]
             plane = self._process(self.raw[pb], pn, out)
             self.free[pb].record(cur)
             yield t0, plane

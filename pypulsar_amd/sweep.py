@@ -71,7 +71,14 @@ class DMSweep(object):
             return max(0, N - self.max_bin)
         return N
 
-    def __call__(self, x, padval=0, trim=True, out=None, stream=None):
+    def __call__(self, x, padval=0, trim=True, out=None, stream=None, n_out=None):
+        """Sweep ``x`` into ``out`` (allocated if None).  ``n_out`` (optional)
+        is the number of plane columns to produce; the default is this grid's
+        trimmed width ``n_out(N, trim)``.  A caller sweeping a slice of a
+        larger grid passes the GLOBAL width (<= this slice's), so every rank
+        of a DM-sharded sweep fills identically shaped rows; columns past a
+        row's own trimmed length are the reference's padded values
+        (dedisperse(trim=False) semantics), never out-of-bounds reads."""
         from .formats.spectra import Spectra, _pad_args
         f32 = None
         if isinstance(x, Spectra):
@@ -84,10 +91,17 @@ class DMSweep(object):
         if x.stride(1) != 1:
             x = x.contiguous()
         N = x.shape[1]
-        n_out = self.n_out(N, trim)
+        if n_out is None:
+            n_out = self.n_out(N, trim)
+        else:
+            n_out = int(n_out)
+            if not 0 <= n_out <= N:
+                raise ValueError("n_out=%d outside [0, N=%d]" % (n_out, N))
         if out is None:
             out = torch.empty((self.D, n_out), dtype=torch.float32, device=x.device)
-        assert out.shape[0] == self.D and out.shape[1] >= n_out and out.stride(1) == 1
+        if out.shape[0] != self.D or out.shape[1] < n_out or out.stride(1) != 1:
+            raise ValueError("out must be [D=%d, >= %d] with unit column stride, got %s / %s"
+                             % (self.D, n_out, tuple(out.shape), tuple(out.stride())))
         if n_out == 0 or N == 0:
             return out
         if x.dtype == torch.uint8 and not _is_int_pad(padval):
@@ -122,10 +136,18 @@ class DMSweep(object):
         self._timed_code = code
 
     def kernel_ms(self):
+        """Sum of the bracketed sweep-kernel durations since the last read."""
+        return self.timing_read()[0]
+
+    def timing_read(self):
+        """(sum of the bracketed sweep-kernel durations in ms, launches) since
+        the last read; every launch has its own HIP event pair on the stream
+        it ran on, recorded without host synchronisation."""
         v = ctypes.c_float()
-        _lib.check(_lib.lib().pdd_sweep_kernel_ms(self._plan(self._timed_code), ctypes.byref(v)),
-                   "pdd_sweep_kernel_ms")
-        return float(v.value)
+        n = ctypes.c_int64()
+        _lib.check(_lib.lib().pdd_sweep_timing_read(self._plan(self._timed_code), ctypes.byref(v),
+                                                    ctypes.byref(n)), "pdd_sweep_timing_read")
+        return float(v.value), int(n.value)
 
     def close(self):
         for p in self._plans.values():
@@ -211,74 +233,145 @@ class GroupedSweep(object):
             pass
 
 
-def execute_plan_grouped(spectra, ddplan, padval=0):
-    """Two-stage DDplan executor in TWO grouped launches per step (trim=True).
+class _Step(object):
+    """Device plans + buffers of one DDstep (DDplanExecutor)."""
+    pass
 
-    Per DDstep: downsample (Spectra.downsample semantics); with subbands,
-    stage 1 forms every pass's subbands at once -- a grouped sweep with one
-    group per subband (its C/nsub channels) whose trials are the passes'
-    subDMs (Spectra.subband shifts + group sum, spectra.py:96-138; pads as
-    there, full length) -- and stage 2 sweeps every pass's DMs at once -- one
-    group per pass, whose channels are that pass's subbands at their centre
-    frequencies (Spectra.dedisperse(dm, trim=True) + channel sum).  Without
-    subbands a step is one plain DMSweep.  Returns [(step, dms, plane)], plane
-    rows = the step's DMs, columns = the common prefix of the per-DM trimmed
-    series (N' - the step's largest delay)."""
-    from .formats.spectra import _pad_args
-    results = []
-    src = spectra.device_data
-    # the raw 8-bit rows when the Spectra still holds them unmodified: the
-    # downsample then reads a quarter of the bytes (exact integer sums)
-    raw8 = getattr(spectra, "_raw8", None)
-    if raw8 is not None and (tuple(raw8.shape) != tuple(src.shape) or raw8.stride(1) != 1):
-        raw8 = None
-    for step in ddplan.DDsteps:
-        # downsampled view of the data (Spectra.downsample semantics, without
-        # copying or modifying the caller's Spectra)
-        dt = spectra.dt * step.downsamp
-        if step.downsamp > 1:
-            C0, N0 = src.shape
-            n_ds = N0 // step.downsamp
-            x = torch.empty((C0, n_ds), dtype=torch.float32, device=src.device)
-            if n_ds and raw8 is not None:
-                call("pdd_downsample_u8", ptr(raw8), C0, N0, raw8.stride(0), step.downsamp, ptr(x),
-                     n_ds, stream_ptr())
-            elif n_ds:
-                call("pdd_downsample", ptr(src), C0, N0, src.stride(0), step.downsamp, ptr(x), n_ds,
-                     stream_ptr())
-        else:
-            x = src
-        calls = step.subband_calls()
-        if calls[0][0] is None:
-            sw = DMSweep(step.DMs, spectra.freqs, dt, cur_dm=spectra.dm, dtype="f32")
-            results.append((step, step.DMs, sw(x, padval=padval, trim=True)))
-            sw.close()
-            continue
-        C, N = x.shape
-        nsub = step.numsub
-        cps = C // nsub
-        freqs = np.asarray(spectra.freqs, dtype=np.float64)
-        subdms = [c[0] for c in calls]
-        ncall = len(calls)
-        # stage 1: [nsub groups][ncall trials][cps channels]
-        t1 = np.stack([_delays.subband_bins(sd, freqs, dt, nsub, cur_dm=spectra.dm)
-                       for sd in subdms])                      # [ncall, C]
-        t1 = t1.reshape(ncall, nsub, cps).transpose(1, 0, 2)    # [nsub, ncall, cps]
-        g1 = GroupedSweep(t1, "f32")
-        mode, pv = _pad_args(x, padval)
-        sub = torch.empty((ncall * nsub, N), dtype=torch.float32, device=x.device)
-        g1(x, N, sub, row_g=1, row_d=nsub, pad_mode=mode, padvals=pv)
-        g1.close()
-        # stage 2: [ncall groups][per-call DMs][nsub subbands at their centres]
-        _, _, ctr = _delays.subband_layout(freqs, nsub)
-        per = len(calls[0][1])
-        assert all(len(c[1]) == per for c in calls)
-        t2 = np.stack([_delays.sweep_table(c[1], ctr, dt, cur_dm=spectra.dm) for c in calls])
-        g2 = GroupedSweep(t2, "f32")
-        n_out = max(0, N - max(0, g2.max_bin))
-        plane = torch.empty((ncall * per, max(n_out, 1)), dtype=torch.float32, device=x.device)
-        if n_out:
-            g2(sub, n_out, plane, row_g=per, row_d=1)
-        g2.close()
-        results.append((step, step.DMs, plane[:, :n_out]))
-    return results
+
+class DDplanExecutor(object):
+    """Two-stage DDplan executor whose delay tables, sweep plans and device
+    buffers are built ONCE per (plan, channel frequencies, dt, N) -- the
+    reference computes its delays on the host per call
+    (formats/spectra.py:126-130, 247-250); here every call of the executor only
+    launches kernels (no host table work, no synchronous hipMemcpy).
+
+    Per DDstep (DDplan2b.py:102-199), ``trim=True``:
+      * downsample by ``step.downsamp`` (Spectra.downsample, spectra.py:329-351;
+        the raw 8-bit rows when the Spectra still holds them: exact integer
+        sums from a quarter of the bytes);
+      * without subbands: one DMSweep over ``step.DMs``;
+      * with subbands: stage 1 forms every pass's subbands in ONE grouped
+        launch -- one group per subband (its C/nsub channels) whose trials are
+        the passes' subDMs (Spectra.subband shifts + group sum,
+        spectra.py:96-138; pads as there, full length) -- and stage 2 sweeps
+        every pass's DMs in ONE grouped launch -- one group per pass, whose
+        channels are that pass's subbands at their centre frequencies
+        (Spectra.dedisperse(dm, padval, trim=True) + channel sum, with the
+        pads of the subbanded data).  subDM_k = loDM + (k+0.5)*dsubDM.
+
+    ``__call__(spectra, padval)`` returns [(step, dms, plane)], plane rows =
+    the step's DMs, columns = the common prefix of the per-DM trimmed series.
+    The planes are the executor's own buffers, overwritten by the next call.
+    """
+
+    def __init__(self, ddplan, freqs, dt, N, cur_dm=0.0, raw8=False, device="cuda"):
+        _lib.require_gpu()
+        self.freqs = np.asarray(freqs, dtype=np.float64)
+        self.C = len(self.freqs)
+        self.N = int(N)
+        self.dt = dt
+        self.cur_dm = cur_dm
+        self.device = torch.device(device)
+        self.steps = []
+        for step in ddplan.DDsteps:
+            s = _Step()
+            s.step = step
+            s.ds = int(step.downsamp)
+            s.dt = dt * s.ds
+            s.n_ds = self.N // s.ds if s.ds > 1 else self.N
+            s.x = (torch.empty((self.C, s.n_ds), dtype=torch.float32, device=self.device)
+                   if s.ds > 1 else None)
+            calls = step.subband_calls()
+            s.two_stage = calls[0][0] is not None
+            if not s.two_stage:
+                # 8-bit rows at full rate go through the exact u16 sweep
+                s.sw = DMSweep(step.DMs, self.freqs, s.dt, cur_dm=cur_dm,
+                               dtype="u8" if (raw8 and s.ds == 1) else "f32")
+                s.n_out = s.sw.n_out(s.n_ds, True)
+                s.plane = torch.empty((s.sw.D, max(s.n_out, 1)), dtype=torch.float32,
+                                      device=self.device)
+                self.steps.append(s)
+                continue
+            nsub = step.numsub
+            cps = self.C // nsub
+            subdms = [c[0] for c in calls]
+            ncall = len(calls)
+            # stage 1: [nsub groups][ncall trials][cps channels]
+            t1 = np.stack([_delays.subband_bins(sd, self.freqs, s.dt, nsub, cur_dm=cur_dm)
+                           for sd in subdms])                      # [ncall, C]
+            t1 = t1.reshape(ncall, nsub, cps).transpose(1, 0, 2)    # [nsub, ncall, cps]
+            s.g1 = GroupedSweep(t1, "f32")
+            s.sub = torch.empty((ncall * nsub, s.n_ds), dtype=torch.float32, device=self.device)
+            # stage 2: [ncall groups][per-call DMs][nsub subbands at their centres]
+            _, _, ctr = _delays.subband_layout(self.freqs, nsub)
+            per = len(calls[0][1])
+            assert all(len(c[1]) == per for c in calls)
+            t2 = np.stack([_delays.sweep_table(c[1], ctr, s.dt, cur_dm=cur_dm) for c in calls])
+            s.g2 = GroupedSweep(t2, "f32")
+            s.nsub, s.ncall, s.per = nsub, ncall, per
+            s.n_out = max(0, s.n_ds - max(0, s.g2.max_bin))
+            s.plane = torch.empty((ncall * per, max(s.n_out, 1)), dtype=torch.float32,
+                                  device=self.device)
+            self.steps.append(s)
+
+    def __call__(self, spectra, padval=0):
+        from .formats.spectra import _pad_args
+        src = spectra.device_data
+        assert tuple(src.shape) == (self.C, self.N), "executor built for a [%d, %d] Spectra" % (
+            self.C, self.N)
+        assert spectra.dm == self.cur_dm and spectra.dt == self.dt
+        raw8 = getattr(spectra, "_raw8", None)
+        if raw8 is not None and (tuple(raw8.shape) != tuple(src.shape) or raw8.stride(1) != 1):
+            raw8 = None
+        results = []
+        for s in self.steps:
+            if s.ds > 1:
+                x = s.x
+                if s.n_ds and raw8 is not None:
+                    call("pdd_downsample_u8", ptr(raw8), self.C, self.N, raw8.stride(0), s.ds,
+                         ptr(x), s.n_ds, stream_ptr())
+                elif s.n_ds:
+                    call("pdd_downsample", ptr(src), self.C, self.N, src.stride(0), s.ds, ptr(x),
+                         s.n_ds, stream_ptr())
+            else:
+                x = src
+            if not s.two_stage:
+                sw = s.sw
+                if sw.dtype == "u8":
+                    if raw8 is not None and _is_int_pad(padval):
+                        x = raw8
+                    else:  # pads that are not 8-bit integers need the float image
+                        if getattr(s, "sw_f32", None) is None:
+                            s.sw_f32 = DMSweep(s.step.DMs, self.freqs, s.dt, cur_dm=self.cur_dm,
+                                               dtype="f32")
+                        sw = s.sw_f32
+                sw(x, padval=padval, trim=True, out=s.plane)
+                results.append((s.step, s.step.DMs, s.plane[:, :s.n_out]))
+                continue
+            mode, pv = _pad_args(x, padval)
+            s.g1(x, s.n_ds, s.sub, row_g=1, row_d=s.nsub, pad_mode=mode, padvals=pv)
+            if s.n_out:
+                # stage 2 pads: those of each pass's subbanded Spectra
+                # (dedisperse(dm, padval) on the subbanded data)
+                mode2, pv2 = _pad_args(s.sub, padval)
+                s.g2(s.sub, s.n_out, s.plane, row_g=s.per, row_d=1, pad_mode=mode2, padvals=pv2)
+            results.append((s.step, s.step.DMs, s.plane[:, :s.n_out]))
+        return results
+
+    def close(self):
+        for s in self.steps:
+            for name in ("sw", "sw_f32", "g1", "g2"):
+                obj = getattr(s, name, None)
+                if obj is not None:
+                    obj.close()
+
+
+def execute_plan_grouped(spectra, ddplan, padval=0):
+    """One-off two-stage DDplan execution (DDplanExecutor built for this
+    Spectra, run once; the returned planes are its own buffers).  Callers
+    that execute the same plan repeatedly keep a DDplanExecutor instead."""
+    ex = DDplanExecutor(ddplan, spectra.freqs, spectra.dt, spectra.numspectra,
+                        cur_dm=spectra.dm, raw8=getattr(spectra, "_raw8", None) is not None)
+    out = ex(spectra, padval=padval)
+    ex.close()
+    return out

@@ -1,0 +1,195 @@
+"""GPU parity at the BASELINE.json workloads, through the product API.
+
+* configs[0]: waterfaller-style Spectra.dedisperse(100, padval, trim=True) of a
+  1024-channel 2^16-sample 8-bit filterbank in get_spectra's layout + the
+  channel sum (bin/waterfaller.py:140), against the oracle;
+* configs[2]: the DDplan2b two-stage executor (4096 -> 64 subbands, res
+  0.5 ms: 2000 DMs, downsample 4, 40 passes x 50) at N = 2^18, sampled rows
+  against oracle subband(64, subDM_k) + per-DM shifted sums;
+* configs[3]: the 4096-channel x 4096-DM (0-1000) sweep at N = 2^18 against
+  oracle rows, the pipelined DMShardedSweep (the bench path) against it, and
+  at the full 2^22 length the size-independent properties (u8 plane == f32
+  plane, rows == the independent single-DM kernel, sharded == direct);
+* configs[4]: the 4096-channel 2048-DM stream of 2^18-spectrum blocks equals
+  the one-shot zero-DM + downsample + sweep, bit for bit.
+
+All inputs are integer-valued 8-bit data with integer pads, so every
+comparison is bit-exact (float32 sums of integers < 2^24), except pad 'mean'
+(1e-5 relative).
+"""
+import numpy as np
+import pytest
+
+from conftest import band, rel_err
+
+DT = 64e-6
+pytestmark = pytest.mark.gpu
+
+
+def _u8(C, N, seed):
+    return np.random.default_rng(seed).integers(0, 256, size=(C, N), dtype=np.uint8)
+
+
+@pytest.mark.parametrize("pad", [0, "mean"])
+def test_config0_waterfaller_dedisperse(gpu, pad):
+    from oracle import spectra_oracle as orc
+    from pypulsar_amd.formats.spectra import Spectra
+    C, N, dm = 1024, 1 << 16, 100.0
+    freqs = band(C)
+    rng = np.random.default_rng(100)
+    x_tc = np.clip(np.round(rng.normal(128, 16, (N, C))), 0, 255).astype(np.uint8)
+    s = Spectra(freqs, DT, x_tc.T)          # filterbank.get_spectra's data.T layout
+    s.dedisperse(dm, padval=pad, trim=True)
+    ser = s.sum_channels().cpu().numpy()
+    got = s.data
+    ref, _ = orc.dedisperse(x_tc.T.astype(np.float64), freqs, DT, dm, padval=pad, trim=True)
+    assert got.shape == ref.shape == (C, N - 1449)
+    want_ser = orc.channel_sum(ref)
+    if pad == 0:
+        np.testing.assert_array_equal(got, ref)
+        np.testing.assert_array_equal(ser.astype(np.float64), want_ser)
+    else:
+        assert rel_err(got, ref) <= 1e-5
+        assert rel_err(ser, want_ser) <= 1e-5
+
+
+def test_config2_two_stage_ddplan(gpu):
+    import torch
+    from oracle import spectra_oracle as orc
+    from pypulsar_amd import delays
+    from pypulsar_amd.formats.spectra import Spectra
+    from pypulsar_amd.sweep import DDplanExecutor
+    from pypulsar_amd.utils.ddplan import Observation
+    C, N = 4096, 1 << 18
+    freqs = band(C)
+    plan = Observation(DT, 1400.0, 300.0, C).gen_ddplan(0.0, 1000.0, 64, 0.5)
+    (step,) = plan.DDsteps
+    calls = step.subband_calls()
+    assert (step.downsamp, len(calls), len(calls[0][1])) == (4, 40, 50)
+    x = _u8(C, N, 7)
+    s = Spectra(freqs, DT, x)
+    ex = DDplanExecutor(plan, freqs, DT, N, raw8=True)
+    for _ in range(2):  # a second call reuses the plans and buffers
+        (got_step, dms, plane) = ex(s)[0]
+    plane = plane.cpu().numpy()
+    ex.close()
+    np.testing.assert_array_equal(dms, step.DMs)
+    # oracle: downsample (channel chunks), then per sampled pass subband(64,
+    # subDM_k), then per sampled DM the shifted channel sum over subbands
+    dt4 = DT * 4
+    xd = np.concatenate([orc.downsample(x[c:c + 512].astype(np.float64), DT, 4)[0]
+                         for c in range(0, C, 512)])
+    n_out = plane.shape[1]
+    _, _, ctr = delays.subband_layout(freqs, 64)
+    assert n_out == N // 4 - int(delays.sweep_table(step.DMs, ctr, dt4).max())
+    for k in (0, 17, 39):
+        subdm, cdms = calls[k]
+        sub, sfreqs = orc.subband(xd, freqs, dt4, 64, subdm=subdm)
+        np.testing.assert_array_equal(sfreqs, ctr)
+        for j in (0, 24, 49):
+            bins = orc.dedisperse_bins(cdms[j], 0.0, sfreqs, dt4)
+            want = orc.shifted_sum(sub, bins)[:n_out]
+            np.testing.assert_array_equal(plane[k * 50 + j].astype(np.float64), want,
+                                          err_msg="pass %d DM %g" % (k, cdms[j]))
+    torch.cuda.synchronize()
+
+
+def test_config3_sweep_oracle_rows(gpu):
+    """4096 ch x 4096 DMs (0-1000) at N = 2^18: sampled rows == oracle, and
+    the pipelined DM-sharded path (one rank, 2 time batches; the bench's
+    DMShardedSweep) == the direct sweep."""
+    import torch
+    from oracle import spectra_oracle as orc
+    from pypulsar_amd.sharding import DMShardedSweep
+    from pypulsar_amd.sweep import DMSweep
+    C, N, D = 4096, 1 << 18, 4096
+    freqs = band(C)
+    dms = np.linspace(0.0, 1000.0, D)
+    x = _u8(C, N, 11)
+    xd = torch.from_numpy(x).cuda()
+    sw = DMSweep(dms, freqs, DT, dtype="u8")
+    plane = sw(xd)
+    n_out = plane.shape[1]
+    assert n_out == N - 14504
+    table = orc.sweep_table(dms, freqs, DT)
+    rows = [0, 1, 1365, 2047, 2048, 2730, 4094, 4095]
+    want = orc.sweep_rows_inside(x, table[rows], n_out)
+    got = plane[rows].cpu().numpy().astype(np.float64)
+    np.testing.assert_array_equal(got, want)
+    sw.close()
+    # the bench path: time-major block, per-batch corner turn + sweep
+    ds = DMShardedSweep(dms, freqs, DT, N, dtype=torch.uint8, n_batches=2, device="cuda")
+    assert (ds.lo, ds.hi, ds.n_out) == (0, D, n_out)
+    part = torch.from_numpy(np.ascontiguousarray(x.T)).cuda().view(2, N // 2, C)
+    ds(part)
+    assert torch.equal(ds.plane(), plane)
+    ds.close()
+
+
+def test_config3_full_length_properties(gpu):
+    """4096 ch x 2^22 samples x 4096 DMs: properties that hold at any size.
+    (a) the exact 8-bit (u16-image) plane equals the float32-image plane;
+    (b) rows equal the independent fused single-DM kernel
+        (Spectra.dedispersed_series, pdd_shift_group_sum);
+    (c) a 64-DM slice swept at the GLOBAL plane width (what a DM-sharded rank
+        does) equals those rows of the full plane."""
+    import torch
+    from pypulsar_amd.formats.spectra import Spectra
+    from pypulsar_amd.sweep import DMSweep
+    C, N, D = 4096, 1 << 22, 4096
+    freqs = band(C)
+    dms = np.linspace(0.0, 1000.0, D)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    x8 = torch.randint(0, 256, (C, N), generator=g, device="cuda", dtype=torch.uint8)
+    sw8 = DMSweep(dms, freqs, DT, dtype="u8")
+    n_out = sw8.n_out(N)
+    assert n_out == 4179800
+    p8 = sw8(x8)
+    sw8.close()
+    xf = x8.float()
+    chunk = 512
+    for lo in range(0, D, chunk):
+        swf = DMSweep(dms[lo:lo + chunk], freqs, DT, dtype="f32")
+        pf = swf(xf, n_out=n_out)
+        assert torch.equal(pf, p8[lo:lo + chunk]), "u8 != f32 plane in DMs [%d, %d)" % (lo, lo + chunk)
+        swf.close()
+        del pf
+    s = Spectra._from_device(freqs, DT, xf)
+    for d in (0, 1000, 2049, 4095):
+        ser = s.dedispersed_series(dms[d], padval=0, trim=True)
+        assert torch.equal(ser[:n_out], p8[d]), "row %d != dedispersed_series" % d
+    sub = DMSweep(dms[100:164], freqs, DT, dtype="u8")
+    assert sub.max_bin < N - n_out  # a low-DM slice, swept at the global width
+    ps = sub(x8, n_out=n_out)
+    assert torch.equal(ps, p8[100:164])
+    sub.close()
+
+
+def test_config4_stream_equals_one_shot(gpu):
+    """configs[4]: 4096-ch 8-bit blocks of 2^18 spectra, zero-DM (float) +
+    downsample 2 + 2048-DM sweep, streamed from pinned host memory ==
+    the one-shot pipeline over the whole stream."""
+    import torch
+    from pypulsar_amd import _lib
+    from pypulsar_amd._lib import call, ptr, stream_ptr
+    from pypulsar_amd.stream import StreamingSweep
+    from pypulsar_amd.sweep import DMSweep
+    C, D, block, ds = 4096, 2048, 1 << 18, 2
+    freqs = band(C)
+    dms = np.linspace(0.0, 1000.0, D)
+    N = 3 * block + 100000
+    x = np.random.default_rng(13).integers(0, 256, size=(N, C), dtype=np.uint8)
+    st = StreamingSweep(dms, freqs, DT, block=block, downsamp=ds)
+    assert st.ov == 7252 * ds
+    chunks = [torch.from_numpy(x[i:i + block]).pin_memory() for i in range(0, N, block)]
+    parts = [p.clone() for _, p in st(chunks)]
+    st.close()
+    got = torch.cat(parts, dim=1)
+    xd = torch.from_numpy(x).cuda()
+    f32 = torch.empty((C, N // ds), dtype=torch.float32, device="cuda")
+    call("pdd_zdm_downsample", ptr(xd), _lib.U8, N, C, C, ds, 1, ptr(f32), f32.stride(0),
+         stream_ptr())
+    want = DMSweep(dms, freqs, DT * ds)(f32)
+    assert got.shape == want.shape
+    assert torch.equal(got, want)

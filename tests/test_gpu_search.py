@@ -100,8 +100,8 @@ def test_sweep_then_search_finds_dispersed_pulse(gpu):
     assert best["Sigma"] > 20
 
 
-@pytest.mark.parametrize("nchunks,last", [(4, 8192), (3, 3000)])
-def test_streaming_search_equals_one_shot(gpu, nchunks, last):
+@pytest.mark.parametrize("nchunks,last,nplanes", [(4, 8192, 0), (3, 3000, 0), (5, 8192, 2)])
+def test_streaming_search_equals_one_shot(gpu, nchunks, last, nplanes):
     """StreamingSearch (blocks searched one behind the sweep, rows continued
     into the next block's plane) finds exactly the candidates of a one-shot
     search of the whole stream's plane, including pulses straddling block
@@ -131,7 +131,10 @@ def test_streaming_search_equals_one_shot(gpu, nchunks, last):
     ss = StreamingSearch(dms, freqs, DT, block=block, downsamp=ds, threshold=5.0, widths=widths,
                          detrendlen=1024)
     chunks = [torch.from_numpy(x[i:i + block]).pin_memory() for i in range(0, N, block)]
-    got = np.concatenate(list(ss(chunks)))
+    # nplanes = 2: the minimum preallocated rotation (block j -> planes[j % 2])
+    planes = ([torch.empty((len(dms), block // ds), dtype=torch.float32, device="cuda")
+               for _ in range(nplanes)] if nplanes else None)
+    got = np.concatenate(list(ss(chunks, planes=planes)))
     ss.close()
     xd = torch.from_numpy(x).cuda()
     f32 = torch.empty((C, N // ds), dtype=torch.float32, device="cuda")

@@ -5,7 +5,8 @@ import pytest
 
 from pypulsar_amd import delays
 from pypulsar_amd.utils import ddplan
-from conftest import band
+from conftest import GOLDEN, band
+import os
 
 DT = 64e-6
 
@@ -94,3 +95,68 @@ def test_ddplan_subband_calls():
     assert all(len(d) == step.DMs_per_prepsub == 50 for _, d in calls)
     assert np.array_equal(np.concatenate([d for _, d in calls]), step.DMs)
     assert calls[0][0] == pytest.approx(0.5 * step.dsubDM)
+
+
+# ---------------------------------------------------------------------------
+# Full BASELINE grids pinned row-for-row against the reference's own bins
+# (tests/golden/make_golden_grids.py records what Spectra.dedisperse /
+# Spectra.subband hand to shift_channels, formats/spectra.py:126-130,247-250)
+# ---------------------------------------------------------------------------
+def _digest(row):
+    import hashlib
+    b = np.ascontiguousarray(np.asarray(row, dtype="<i4")).tobytes()
+    return np.frombuffer(hashlib.blake2b(b, digest_size=8).digest(), dtype="<u8")[0]
+
+
+@pytest.fixture(scope="module")
+def grids():
+    return np.load(os.path.join(GOLDEN, "golden_grids.npz"), allow_pickle=False)
+
+
+def _check_rows(g, key, table):
+    table = delays.to_int32(table)
+    assert table.shape[0] == len(g[key + "_digest"])
+    np.testing.assert_array_equal(table.max(axis=1), g[key + "_max"])
+    got = np.array([_digest(r) for r in table], dtype="<u8")
+    bad = np.nonzero(got != g[key + "_digest"])[0]
+    assert bad.size == 0, "%s: %d rows differ from the reference (first %s)" % (key, bad.size,
+                                                                                bad[:5])
+    np.testing.assert_array_equal(table[0], g[key + "_row0"])
+    np.testing.assert_array_equal(table[-1], g["%s_row%d" % (key, table.shape[0] - 1)])
+
+
+@pytest.mark.parametrize("key,fkey", [("cfg0", "freqs1024"), ("cfg1", "freqs1024"),
+                                      ("cfg3", "freqs4096"), ("ns", "freqs4096"),
+                                      ("cfg4", "freqs4096")])
+def test_baseline_grid_tables_match_reference(grids, key, fkey):
+    """configs[0], [1], [3], [4] and the north-star grid: every row of the
+    host sweep table equals the reference's dedisperse bins."""
+    g = grids
+    tab = delays.sweep_table(g[key + "_dms"], g[fkey], float(g[key + "_dt"]))
+    _check_rows(g, key, tab)
+
+
+def test_config2_two_stage_tables_match_reference(grids):
+    """configs[2] (DDplan2b 4096 -> 64 subbands, res 0.5 ms): the plan's
+    subband passes (subDM_k), the stage-1 tables (Spectra.subband bins) and
+    the stage-2 tables (dedisperse bins on the subband centres) the
+    DDplanExecutor builds are the reference's, row for row."""
+    from pypulsar_amd.utils.ddplan import Observation
+    g = grids
+    freqs = g["freqs4096"]
+    plan = Observation(64e-6, 1400.0, 300.0, 4096).gen_ddplan(0.0, 1000.0, 64, 0.5)
+    assert len(plan.DDsteps) == 1
+    st = plan.DDsteps[0]
+    ds, ncall, per, dsub, lo, ddm = g["cfg2_meta"]
+    assert (st.downsamp, st.numprepsub, st.DMs_per_prepsub) == (ds, ncall, per)
+    calls = st.subband_calls()
+    subdms = np.array([c[0] for c in calls])
+    np.testing.assert_array_equal(subdms, g["cfg2s1_dms"])
+    np.testing.assert_array_equal(np.concatenate([c[1] for c in calls]), g["cfg2s2_dms"])
+    dt = 64e-6 * st.downsamp
+    t1 = np.stack([delays.subband_bins(sd, freqs, dt, 64) for sd in subdms])
+    _check_rows(g, "cfg2s1", t1)
+    _, _, ctr = delays.subband_layout(freqs, 64)
+    np.testing.assert_array_equal(ctr, g["cfg2_ctr"])
+    t2 = delays.sweep_table(np.concatenate([c[1] for c in calls]), ctr, dt)
+    _check_rows(g, "cfg2s2", t2)

@@ -138,3 +138,15 @@ def test_downsample_then_dedisperse(golden):
     d, dt = orc.downsample(x, DT, 4)
     dd, _ = orc.dedisperse(d, golden["sw_freqs"], dt, 200.0, trim=True)
     np.testing.assert_array_equal(orc.channel_sum(dd), golden["dsdd_series"])
+
+
+def test_sweep_rows_inside_equals_sweep_plane():
+    """The fast pad-free row restatement equals the per-channel shifted sum."""
+    from oracle import spectra_oracle as orc
+    rng = np.random.default_rng(9)
+    x = rng.integers(0, 256, size=(32, 700), dtype=np.uint8)
+    foff = -300.0 / 32
+    freqs = 1550.0 + foff / 2 + foff * np.arange(32)
+    tab = orc.sweep_table(np.linspace(0, 30, 7), freqs, 64e-6)
+    want = orc.sweep_plane(x.astype(np.float64), tab)
+    np.testing.assert_array_equal(orc.sweep_rows_inside(x, tab, want.shape[1]), want)

@@ -49,7 +49,7 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        C, N = 16, 1000
+        C, N, NB = 16, 1000, 2400
         freqs = _band(C)
         dms = np.linspace(0.0, 40.0, 11)
         from oracle import spectra_oracle as orc
@@ -79,19 +79,36 @@ def _worker(rank, world, port, q):
         cands = sharding.dm_sharded_search(xs, (C, N), torch.float32, dms, freqs, DT, n_out,
                                            sweep_fn=_oracle_sweep(freqs, n_out),
                                            search_fn=search_fn)
-        # all-gather exchange: each rank holds 1/world of the time-major block
-        xt = _data(C, N).T.copy()  # [N, C]
-        nr = -(-N // world)
-        xt = np.concatenate([xt, np.zeros((nr * world - N, C), np.float32)])
-        part = torch.from_numpy(xt[rank * nr:(rank + 1) * nr].copy())
-        (lo, hi), mine = sharding.dm_sharded_sweep_ag(
-            part, dms, freqs, DT, n_out, sweep_fn=_oracle_sweep(freqs, n_out),
-            to_cm=lambda b: b[:N].t().contiguous())
+        # pipelined DM sharding (DMShardedSweep): per-rank H2D slices of every
+        # time batch, all-gathered batch by batch; planes resident (ag) or
+        # gathered to rank 0 batch by batch (agg); DM slices work-weighted
+        xt = torch.from_numpy(_data(C, NB).T.copy())  # [NB, C] time-major
+        work = np.r_[np.ones(5), np.full(len(dms) - 5, 0.5)]
+
+        def to_cm(src_tc, dst_cm):
+            dst_cm.copy_(src_tc.t())
+
+        def sweep_fn(xv, sub, out, n_cols):
+            tab = orc.sweep_table(sub, freqs, DT)
+            out.copy_(torch.from_numpy(orc.sweep_plane(xv.numpy().astype(np.float64), tab,
+                                                       n_out=n_cols).astype(np.float32)))
+        res = {}
+        for gather in (False, True):
+            ds = sharding.DMShardedSweep(dms, freqs, DT, NB, dtype=torch.float32, n_batches=2,
+                                         work=work, gather=gather, to_cm=to_cm,
+                                         sweep_fn=sweep_fn)
+            part = sharding.split_block(xt, 2, world, rank)
+            for _ in range(2):  # a second step reuses every buffer
+                ds(part)
+            res[gather] = (ds.lo, ds.hi, ds.plane().numpy(), ds.slices)
         ag = [None] * world
-        dist.all_gather_object(ag, (lo, hi, None if mine is None else mine.numpy()))
+        dist.all_gather_object(ag, res[False][:3])
+        # plane gather into a preallocated plane (no concatenation)
+        g = sharding.gather_planes(torch.from_numpy(res[False][2]), res[False][3])
         if rank == 0:
-            q.put(("ag", np.concatenate([p for _, _, p in sorted(ag, key=lambda a: a[0])
-                                         if p is not None])))
+            q.put(("ag", np.concatenate([p for _, _, p in sorted(ag, key=lambda a: a[0])])))
+            q.put(("agg", res[True][2]))
+            q.put(("gp", g.numpy()))
             q.put(("dm", plane.numpy()))
             q.put(("tb", np.concatenate(parts, axis=1)))
             q.put(("sp", cands))
@@ -108,7 +125,7 @@ def test_sharded_sweeps_equal_one_shot(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=240) for _ in range(4))
+    got = dict(q.get(timeout=240) for _ in range(6))
     for p in procs:
         p.join(timeout=240)
         assert p.exitcode == 0
@@ -119,7 +136,11 @@ def test_sharded_sweeps_equal_one_shot(world):
     want = orc.sweep_plane(_data(C, N).astype(np.float64), tab)
     np.testing.assert_array_equal(got["dm"].astype(np.float64), want)
     np.testing.assert_array_equal(got["tb"], want)
-    np.testing.assert_array_equal(got["ag"].astype(np.float64), want)
+    # the pipelined DM-sharded sweep: block of NB spectra, 2 time batches
+    want_b = orc.sweep_plane(_data(C, 2400).astype(np.float64), tab)
+    np.testing.assert_array_equal(got["ag"].astype(np.float64), want_b)
+    np.testing.assert_array_equal(got["agg"].astype(np.float64), want_b)
+    np.testing.assert_array_equal(got["gp"].astype(np.float64), want_b)
     # sharded search == search of the one-shot plane
     from oracle import search_oracle as so
     xs = _data(C, N)
