@@ -10,10 +10,13 @@ without a GPU or without libpdd.so the methods raise.
 Documented differences from the reference:
   * float32 on device instead of float64 (parity: integer-valued data and
     integer pads are bit-exact; otherwise 1e-5 relative, SURVEY.md §8(c));
-  * ``.data`` is a float64 host *snapshot* (a device->host copy), so writing
-    into ``spectra.data[...]`` does not change the Spectra: use
-    ``spectra[key] = value`` (``__setitem__``) or assign ``spectra.data = arr``;
-  * ``get_chan``/``get_spectrum`` likewise return host copies.
+  * ``.data`` is a float64 host copy (one device->host transfer per access)
+    that WRITES THROUGH: ``s.data[...] = v``, ``chan = s.get_chan(i);
+    chan[:] = v`` and in-place arithmetic on those arrays or their slices
+    upload the modified array back to the device, like the reference's views
+    into its own ndarray (formats/spectra.py:42-52); a view taken before the
+    Spectra was modified again (dedisperse, trim, ...) raises instead of
+    overwriting the newer data.
 """
 import copy
 
@@ -119,6 +122,46 @@ def _pad_args(x, padval):
     return _lib.PAD_VALUE, pv
 
 
+class HostView(np.ndarray):
+    """float64 host copy of a Spectra's device data whose writes go back to
+    the device: ``__setitem__`` and in-place ufuncs on it -- or on any slice
+    of it (they share its memory) -- upload the whole copy.  Reference idiom
+    kept: ``chan = s.get_chan(i); chan[:] = v`` changes channel i
+    (formats/spectra.py:48-52: get_chan returns a view into self.data)."""
+
+    def __array_finalize__(self, obj):
+        self._root = getattr(obj, "_root", None)
+
+    def _push(self):
+        root = self._root
+        if root is None:
+            return
+        s, version = root._owner
+        if s._version != version:
+            raise RuntimeError("Spectra was modified after this view of its data was taken; "
+                               "take a new view (s.data / get_chan / get_spectrum)")
+        s._upload_host(np.asarray(root).view(np.ndarray))
+        root._owner = (s, s._version)
+
+    def __setitem__(self, key, value):
+        super(HostView, self).__setitem__(key, value)
+        self._push()
+
+    def __array_ufunc__(self, ufunc, method, *inputs, **kwargs):
+        args = [np.asarray(a).view(np.ndarray) if isinstance(a, HostView) else a for a in inputs]
+        outs = kwargs.get("out")
+        if outs:
+            kwargs["out"] = tuple(np.asarray(o).view(np.ndarray) if isinstance(o, HostView) else o
+                                  for o in outs)
+        res = getattr(ufunc, method)(*args, **kwargs)
+        if outs:
+            for o in outs:
+                if isinstance(o, HostView):
+                    o._push()
+            return outs[0] if len(outs) == 1 else outs
+        return res
+
+
 def _bins_dev(bins, device):
     return torch.from_numpy(_delays.to_int32(bins)).to(device)
 
@@ -131,6 +174,7 @@ class Spectra(object):
         assert len(freqs) == self.numchans
         self.freqs = freqs
         self._x, self._raw8 = upload_f32(data)
+        self._version = 0
         self.dt = dt
         self.starttime = starttime
         self.dm = 0  # the reference ignores the dm argument (spectra.py:37)
@@ -146,6 +190,7 @@ class Spectra(object):
         assert len(freqs) == self.numchans
         self.freqs = freqs
         self._x, self._raw8 = x, None
+        self._version = 0
         self.dt = dt
         self.starttime = starttime
         self.dm = 0
@@ -159,19 +204,32 @@ class Spectra(object):
 
     @property
     def data(self):
-        return self._x.to(torch.float64).cpu().numpy()
+        """float64 host copy of the data that writes through to the device
+        (HostView)."""
+        v = self._x.to(torch.float64).cpu().numpy().view(HostView)
+        v._root = v
+        v._owner = (self, self._version)
+        return v
 
     @data.setter
     def data(self, value):
         self._x, self._raw8 = upload_f32(value)
         self.numchans, self.numspectra = self._x.shape
+        self._version = getattr(self, "_version", 0) + 1
+
+    def _upload_host(self, arr):
+        """Write a full [numchans, numspectra] host array back (HostView)."""
+        assert arr.shape == tuple(self._x.shape)
+        self._x.copy_(torch.from_numpy(np.ascontiguousarray(arr, dtype=np.float32)))
+        self._raw8 = None
 
     def _set(self, x):
         self._x = x
         self._raw8 = None
+        self._version = getattr(self, "_version", 0) + 1
 
     def __str__(self):
-        return str(self.data)
+        return str(np.asarray(self.data))
 
     def __getitem__(self, key):
         return self.data[key]
@@ -181,6 +239,7 @@ class Spectra(object):
             value = torch.as_tensor(np.asarray(value, dtype=np.float32))
         self._x[key] = value.to(device=self._x.device, dtype=torch.float32)
         self._raw8 = None
+        self._version = getattr(self, "_version", 0) + 1
 
     def get_chan(self, channum):
         return self.data[channum, :]
@@ -190,6 +249,7 @@ class Spectra(object):
 
     def __deepcopy__(self, memo):
         other = copy.copy(self)
+        other._version = 0
         other._x = self._x.clone()
         other._raw8 = None if self._raw8 is None else self._raw8.clone()
         other.freqs = copy.deepcopy(self.freqs, memo)

@@ -63,7 +63,7 @@ class DMSweep(object):
         _lib.check(_lib.lib().pdd_sweep_plan_info(self._plan(code), a.ctypes.data_as(ctypes.c_void_p)),
                    "pdd_sweep_plan_info")
         keys = ("D", "C", "dms_per_block", "samples_per_block", "lds_bytes", "max_bin", "min_bin",
-                "chans_per_chunk")
+                "variant")
         return dict(zip(keys, (int(v) for v in a)))
 
     def n_out(self, N, trim=True):

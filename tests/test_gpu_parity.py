@@ -370,3 +370,36 @@ def test_deepcopy_independent(S):
     t = copy.deepcopy(s)
     t.dedisperse(500.0)
     np.testing.assert_array_equal(s.data, x.astype(np.float64))
+
+
+# Every tiling the plan can choose, reached by a grid whose per-trial-block
+# shift span forces it (pdd_sweep.hip kF32Variants / kU8Variants, best first),
+# each checked against the oracle.  dDM ladder: span ~ (DB - 1) * 14.5 * dDM
+# bins at the bottom channel.
+LADDER = {"f32": [0.5, 2.0, 4.5, 12.0, 40.0], "u8": [0.5, 2.0, 4.5, 12.0, 40.0]}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["f32", "u8"])
+def test_sweep_variant_ladder(gpu, dtype):
+    import torch
+    from oracle import spectra_oracle as orc
+    from pypulsar_amd.sweep import DMSweep
+    C, N, D = 32, 49152, 64
+    freqs = band(C)
+    x = u8_data(C, N, 21)
+    xd = torch.from_numpy(x).cuda()
+    if dtype == "f32":
+        xd = xd.float()
+    code = 1 if dtype == "u8" else 0
+    seen = []
+    for ddm in LADDER[dtype]:
+        dms = np.arange(D) * ddm
+        sw = DMSweep(dms, freqs, DT, dtype=dtype)
+        v = sw.info(code)["variant"]
+        plane = sw(xd).cpu().numpy().astype(np.float64)
+        want = orc.sweep_plane(x.astype(np.float64), orc.sweep_table(dms, freqs, DT))
+        np.testing.assert_array_equal(plane, want, err_msg="dDM %g (variant %d)" % (ddm, v))
+        sw.close()
+        seen.append(v)
+    assert seen == sorted(seen) and sorted(set(seen)) == list(range(len(LADDER[dtype]))), seen
