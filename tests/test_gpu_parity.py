@@ -374,9 +374,11 @@ def test_deepcopy_independent(S):
 
 # Every tiling the plan can choose, reached by a grid whose per-trial-block
 # shift span forces it (pdd_sweep.hip kF32Variants / kU8Variants, best first),
-# each checked against the oracle.  dDM ladder: span ~ (DB - 1) * 14.5 * dDM
-# bins at the bottom channel.
-LADDER = {"f32": [0.5, 2.0, 4.5, 12.0, 40.0], "u8": [0.5, 2.0, 4.5, 12.0, 40.0]}
+# each checked against the oracle: (dDM, expected variant index).  Span ~
+# (DB - 1) * 14.5 * dDM bins at the bottom channel.  u8 index 3 (the u16
+# VALU kernel) is only chosen for grouped 8-bit sweeps: test below.
+LADDER = {"f32": [(0.5, 0), (2.0, 1), (4.5, 2), (12.0, 3), (40.0, 4)],
+          "u8": [(0.5, 0), (1.6, 1), (3.0, 2), (5.0, 4), (12.0, 5), (40.0, 6)]}
 
 
 @pytest.mark.gpu
@@ -392,14 +394,41 @@ def test_sweep_variant_ladder(gpu, dtype):
     if dtype == "f32":
         xd = xd.float()
     code = 1 if dtype == "u8" else 0
-    seen = []
-    for ddm in LADDER[dtype]:
+    for ddm, want_v in LADDER[dtype]:
         dms = np.arange(D) * ddm
         sw = DMSweep(dms, freqs, DT, dtype=dtype)
         v = sw.info(code)["variant"]
+        assert v == want_v, "dDM %g chose variant %d, expected %d" % (ddm, v, want_v)
         plane = sw(xd).cpu().numpy().astype(np.float64)
         want = orc.sweep_plane(x.astype(np.float64), orc.sweep_table(dms, freqs, DT))
         np.testing.assert_array_equal(plane, want, err_msg="dDM %g (variant %d)" % (ddm, v))
         sw.close()
-        seen.append(v)
-    assert seen == sorted(seen) and sorted(set(seen)) == list(range(len(LADDER[dtype]))), seen
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pad", [0, 7, "rotate"])
+def test_grouped_u8_sweep(gpu, pad):
+    """Grouped 8-bit sweep (u16-eighths VALU kernel, kU8Variants[3]): two
+    channel groups with their own tables, against per-group oracle planes."""
+    import torch
+    from pypulsar_amd import _lib
+    from pypulsar_amd.sweep import GroupedSweep
+    C, N, G = 24, 6000, 2
+    freqs = band(C)
+    x = u8_data(G * C, N, 22)
+    tabs = np.stack([orc.sweep_table(np.linspace(0, 30, 10), freqs, DT),
+                     orc.sweep_table(np.linspace(5, 60, 10), freqs, DT)])
+    gs = GroupedSweep(tabs, "u8")
+    n_out = N  # untrimmed: the last columns read pads / wrapped samples
+    out = torch.zeros((G * 10, n_out), dtype=torch.float32, device="cuda")
+    if pad == "rotate":
+        mode, pv = _lib.PAD_ROTATE, None
+    else:
+        mode, pv = _lib.PAD_VALUE, torch.full((G * C,), float(pad), device="cuda")
+    gs(torch.from_numpy(x).cuda(), n_out, out, row_g=10, row_d=1, pad_mode=mode, padvals=pv)
+    got = out.cpu().numpy().astype(np.float64)
+    for g in range(G):
+        want = orc.sweep_plane(x[g * C:(g + 1) * C].astype(np.float64), tabs[g], padval=pad,
+                               n_out=n_out)
+        np.testing.assert_array_equal(got[g * 10:(g + 1) * 10], want)
+    gs.close()
