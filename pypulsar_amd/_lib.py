@@ -13,6 +13,10 @@ import torch  # noqa: F401  (load torch's HIP runtime before libpdd.so)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpdd.so")
+# developer builds (-DPDD_SWEEP_DEV, scripts/build_dev.sh) are loaded from
+# PDD_DEV_LIB for timing experiments; production runs never set it
+if os.environ.get("PDD_DEV_LIB"):
+    LIB_PATH = os.environ["PDD_DEV_LIB"]
 
 # element types / modes (include/pdd.h)
 F32, U8, U16 = 0, 1, 2

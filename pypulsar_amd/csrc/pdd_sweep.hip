@@ -28,6 +28,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "pdd_internal.h"
@@ -879,6 +880,14 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
 #undef IL_TILE_SETUP
 
 // ------------------------------------------------------------------ MFMA sweep (8-bit data)
+// EXPERIMENTAL, developer builds only (-DPDD_SWEEP_DEV, PDD_SWEEP_MX=1):
+// correct (oracle-exact on the variant ladder and the config-3 grid) but
+// measured SLOWER than the u16 VALU kernel on BASELINE configs[3]
+// (28.6 vs 38.1 T adds/s; DESIGN.md §3 "MFMA sweep"): with 16-trial tiles
+// (register-limited: 136 i32 accumulators per wave) it stages 0.11 B of
+// window per add against 0.083 for the 48-trial u16 tiles, and the LDS-DMA
+// staging path (~80-130 CU-cycles per KiB) is what binds both kernels.
+#ifdef PDD_SWEEP_DEV
 // For 8-bit input the channel sum runs on the matrix cores (gfx950 i8 MFMA),
 // not on the VALU.  Per DM trial and 16 output times, one
 //     v_mfma_i32_16x16x64_i8  C[m][n] += sum_k A[m][k] * B[k][n]
@@ -907,24 +916,34 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
 constexpr int kMxCh = 64;     // channels per chunk (MFMA K)
 constexpr int kMxRec = 192;   // metadata bytes per (trial, chunk): 64 phases + 32 offset pairs
 
-// R8[c][j] = X(c, base + j) ^ 0x80 with the reference pads (value / rotate)
-// for j < nR8 (a multiple of 16); rows C..Cpad-1 = 0 (int8 0: contribute 0).
+// i8 image in the kernel's LDS layout, so every staging DMA reads 1 KiB of
+// contiguous global memory:  R8g[grp][row][c16][16 B] holds the samples
+// X(16 grp + c16, base + 16 row + i) ^ 0x80, i < 16 (x - 128 as int8), with the
+// reference pads (value / rotate) outside [0, N); channels >= C are 0 (they
+// contribute 0).  One thread writes 4 rows of one channel (64 input bytes).
 __global__ __launch_bounds__(256) void k_prep8(const uint8_t* __restrict__ x, int64_t ld, int64_t N,
-                                               int C, int64_t base, int64_t nR8, int pad_mode,
+                                               int C, int64_t base, int64_t nrows, int pad_mode,
                                                const float* __restrict__ padvals,
-                                               uint8_t* __restrict__ R8, int fast) {
-  const int c = blockIdx.y;
-  const int64_t j0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 16;
-  if (j0 >= nR8) return;
-  uint4 o;
-  if (c >= C) {
-    o = make_uint4(0u, 0u, 0u, 0u);
-  } else {
-    const uint8_t* row = x + (int64_t)c * ld;
-    const int64_t s0 = base + j0;
+                                               uint8_t* __restrict__ R8g, int fast) {
+  const int grp = blockIdx.y;
+  const int c16 = threadIdx.x & 15;
+  const int c = grp * 16 + c16;
+  const int64_t row0 = ((int64_t)blockIdx.x * 16 + (threadIdx.x >> 4)) * 4;
+  uint8_t* dst = R8g + ((int64_t)grp * nrows) * 256 + c16 * 16;
+  uint4 o[4];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int64_t row = row0 + rr;
+    if (row >= nrows) break;
+    if (c >= C) {
+      o[rr] = make_uint4(0u, 0u, 0u, 0u);
+      continue;
+    }
+    const uint8_t* xr = x + (int64_t)c * ld;
+    const int64_t s0 = base + 16 * row;
     if (fast && s0 >= 0 && s0 + 16 <= N) {
-      const uint4 v = *reinterpret_cast<const uint4*>(row + s0);
-      o = make_uint4(v.x ^ 0x80808080u, v.y ^ 0x80808080u, v.z ^ 0x80808080u, v.w ^ 0x80808080u);
+      const uint4 v = *reinterpret_cast<const uint4*>(xr + s0);
+      o[rr] = make_uint4(v.x ^ 0x80808080u, v.y ^ 0x80808080u, v.z ^ 0x80808080u, v.w ^ 0x80808080u);
     } else {
       const uint32_t pv = (pad_mode == PDD_PAD_VALUE) ? (uint32_t)padvals[c] : 0u;
       uint32_t wv[4];
@@ -935,17 +954,19 @@ __global__ __launch_bounds__(256) void k_prep8(const uint8_t* __restrict__ x, in
         for (int i = 0; i < 4; ++i) {
           const int64_t s = s0 + 4 * q + i;
           uint32_t v;
-          if (s >= 0 && s < N) v = row[s];
-          else if (pad_mode == PDD_PAD_ROTATE) v = row[wrap_mod(s, N)];
+          if (s >= 0 && s < N) v = xr[s];
+          else if (pad_mode == PDD_PAD_ROTATE) v = xr[wrap_mod(s, N)];
           else v = pv;
           acc |= ((v ^ 0x80u) & 0xffu) << (8 * i);
         }
         wv[q] = acc;
       }
-      o = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+      o[rr] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
     }
   }
-  *reinterpret_cast<uint4*>(R8 + (int64_t)c * nR8 + j0) = o;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr)
+    if (row0 + rr < nrows) *reinterpret_cast<uint4*>(dst + (row0 + rr) * 256) = o[rr];
 }
 
 // one 1 KiB LDS-DMA wave-instruction: lane l copies 16 B from src (its own
@@ -964,6 +985,7 @@ __device__ __forceinline__ void dma16(uint32_t lds_dst, const void* src) {
 }
 
 typedef int i32x4_mx __attribute__((ext_vector_type(4)));
+typedef i32x4_mx i32x4_mx_acc;
 typedef int i32x2_mx __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) i32x2_mx lds_i32x2_mx;
 typedef __attribute__((address_space(3))) i32x4_mx lds_i32x4_mx;
@@ -973,19 +995,68 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8_mx;
 
 __host__ __device__ constexpr int mx_scr_bytes(int S) { return (16 * (S + 1) + 32) * 32; }
 
+// ds_read_b64_tr_b8 through asm: the compiler neither waits for it nor folds a
+// prefetch ring back into one register set; the caller waits with mx_wait.
+template <int OFF>
+__device__ __forceinline__ void mx_tr8(i32x2_mx& r, uint32_t addr) {
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF) : "memory");
+}
+// s_waitcnt lgkmcnt(N) tied to the two operand halves it releases
+template <int N>
+__device__ __forceinline__ void mx_wait(i32x2_mx& a, i32x2_mx& b) {
+  static_assert(N >= 0 && N <= 15, "lgkmcnt field");
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
+}
+
+// One step of the MFMA sequence (I = trial * (S + 1) + subtile): wait for
+// its operands, issue the MFMA, refill the ring PF steps ahead.  Expanded by
+// a fold over an integer sequence so every index is a compile-time constant.
+template <int S, int DPW, int PF>
+struct MxSeq {
+  static constexpr int NM = DPW * (S + 1), NSL = PF + 1;
+  template <int I>
+  static __device__ __forceinline__ void read(i32x2_mx* r0, i32x2_mx* r1, const uint32_t* a0,
+                                              const uint32_t* a1) {
+    mx_tr8<256 * (I % (S + 1))>(r0[I % NSL], a0[I / (S + 1)]);
+    mx_tr8<256 * (I % (S + 1))>(r1[I % NSL], a1[I / (S + 1)]);
+  }
+  template <int I>
+  static __device__ __forceinline__ void step(i32x2_mx* r0, i32x2_mx* r1, i32x4_mx_acc* acc,
+                                              const i32x4_mx_acc* B, const uint32_t* a0,
+                                              const uint32_t* a1) {
+    constexpr int ahead = (NM - 1 - I) < (PF - 1) ? (NM - 1 - I) : (PF - 1);
+    mx_wait<2 * ahead>(r0[I % NSL], r1[I % NSL]);
+    const i32x4_mx_acc A = (i32x4_mx_acc){r0[I % NSL].x, r0[I % NSL].y, r1[I % NSL].x, r1[I % NSL].y};
+    acc[I] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B[I / (S + 1)], acc[I], 0, 0, 0);
+    if constexpr (I + PF < NM) read<I + PF>(r0, r1, a0, a1);
+  }
+  template <int... Is>
+  static __device__ __forceinline__ void prologue(std::integer_sequence<int, Is...>, i32x2_mx* r0,
+                                                  i32x2_mx* r1, const uint32_t* a0,
+                                                  const uint32_t* a1) {
+    (read<Is>(r0, r1, a0, a1), ...);
+  }
+  template <int... Is>
+  static __device__ __forceinline__ void run(std::integer_sequence<int, Is...>, i32x2_mx* r0,
+                                             i32x2_mx* r1, i32x4_mx_acc* acc, const i32x4_mx_acc* B,
+                                             const uint32_t* a0, const uint32_t* a1) {
+    (step<Is>(r0, r1, acc, B, a0, a1), ...);
+  }
+};
+
 template <int NW, int DPW, int S, int NBUF>
 __global__ __launch_bounds__(NW * 64) void k_sweep_mx(
-    const uint8_t* __restrict__ R8, int64_t nR8, int nchunk, const uint8_t* __restrict__ meta,
+    const uint8_t* __restrict__ R8, int64_t nR8, int nchunk, const uint8_t* __restrict__ meta,  // nR8: rows per group
     const uint16_t* __restrict__ win, const uint8_t* __restrict__ rows, int rows_max,
     float* __restrict__ out, int64_t ld_out, int D, int64_t t_base, int64_t t_end, int n_dblk,
-    int corr) {
+    int corr, int dbg) {
   constexpr int DB = NW * DPW;
   constexpr int TT = 16 * S;
   constexpr int META_B = DB * kMxRec;
   static_assert(META_B % 1024 == 0, "metadata must be whole 1 KiB DMA pieces");
   extern __shared__ __attribute__((aligned(16))) uint8_t smx[];
-  const int Cpad = nchunk * kMxCh;
-  const int WIN_B = (2 * Cpad + 15) & ~15;
+  const int ngrp = nchunk * 4;            // 16-channel groups
+  const int WIN_B = (2 * ngrp + 15) & ~15;
   const int ROWS_B = (4 * nchunk + 15) & ~15;
   const int GB = rows_max * 256;         // bytes per 16-channel group
   const int BUF = 4 * GB + META_B;       // bytes per chunk buffer
@@ -994,14 +1065,24 @@ __global__ __launch_bounds__(NW * 64) void k_sweep_mx(
 
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int dblk = blockIdx.x % n_dblk;
-  const int64_t t0 = (int64_t)(blockIdx.x / n_dblk) * TT;
+  // XCD-aware tile order: blocks b and b + 8 share an XCD; XCD x owns the
+  // trial blocks [x R, (x + 1) R) (R = n_dblk rounded up to 8, / 8) and walks
+  // them trial block fastest, so its ~32 resident tiles are CONSECUTIVE trial
+  // blocks of one time tile, whose channel windows overlap (adjacent trial
+  // blocks' shifts differ by about one span): the staging is served from the
+  // XCD's L2 instead of the Infinity Cache.
+  const int R = (n_dblk + 7) / 8;
+  const int xcd = blockIdx.x % 8, kx = blockIdx.x / 8;
+  const int dblk = xcd * R + kx % R;
+  if (dblk >= n_dblk) return;  // padding of the trial-block ranges
+  const int64_t t0 = (int64_t)(kx / R) * TT;
 
-  // per-block tables: window starts (u16 per channel) and rows per group
+  // per-block tables: window start of every 16-channel group (u16, in
+  // samples, a multiple of 16) and staged rows per group
   {
-    const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(win + (int64_t)dblk * Cpad);
-    uint32_t* wdst = reinterpret_cast<uint32_t*>(smx);
-    for (int i = threadIdx.x; i < Cpad / 2; i += NW * 64) wdst[i] = wsrc[i];
+    const uint16_t* wsrc = win + (int64_t)dblk * ngrp;
+    uint16_t* wdst = reinterpret_cast<uint16_t*>(smx);
+    for (int i = threadIdx.x; i < ngrp; i += NW * 64) wdst[i] = wsrc[i];
     const uint32_t* rsrc = reinterpret_cast<const uint32_t*>(rows + (int64_t)dblk * nchunk * 4);
     uint32_t* rdst = reinterpret_cast<uint32_t*>(smx + WIN_B);
     for (int i = threadIdx.x; i < nchunk; i += NW * 64) rdst[i] = rsrc[i];
@@ -1010,17 +1091,19 @@ __global__ __launch_bounds__(NW * 64) void k_sweep_mx(
 
   const uint8_t* meta_b = meta + (int64_t)dblk * nchunk * META_B;
   auto issue = [&](int k) -> int {
+    if (dbg & 1) return 0;  // dev: no staging (timing only, wrong results)
     const uint32_t bufb = buf0 + (uint32_t)((k % NBUF) * BUF);
     int n = 0, pi = 0;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const int ch = k * kMxCh + g * 16 + (lane & 15);
-      const int rg = *(const lds_u8_mx*)(uintptr_t)(lds0 + WIN_B + k * 4 + g);
-      const int ws = *(const lds_u16_mx*)(uintptr_t)(lds0 + 2 * ch);
-      const uint8_t* src = R8 + (int64_t)ch * nR8 + t0 + ws + 16 * (lane >> 4);
+      const int grp = k * 4 + g;
+      const int rg = __builtin_amdgcn_readfirstlane(*(const lds_u8_mx*)(uintptr_t)(lds0 + WIN_B + grp));
+      const int ws = __builtin_amdgcn_readfirstlane(*(const lds_u16_mx*)(uintptr_t)(lds0 + 2 * grp));
+      // 4 rows (1 KiB, contiguous) per piece
+      const uint8_t* src = R8 + ((int64_t)grp * nR8 + (t0 + ws) / 16) * 256 + 16 * lane;
       for (int pg = 0; pg < (rg >> 2); ++pg, ++pi)
         if (pi % NW == w) {
-          dma16(bufb + (uint32_t)(g * GB + pg * 1024), src + 64 * pg);
+          dma16(bufb + (uint32_t)(g * GB + pg * 1024), src + 1024 * pg);
           ++n;
         }
     }
@@ -1064,29 +1147,33 @@ __global__ __launch_bounds__(NW * 64) void k_sweep_mx(
       for (int i = NBUF - 1; i > 0; --i) hist[i] = hist[i - 1];
       hist[0] = n;
     }
+    if (dbg & 2) continue;  // dev: no compute (timing only, wrong results)
     const uint32_t bufb = buf0 + (uint32_t)((k % NBUF) * BUF);
+    // per trial: B (phase one-hot) and the two row addresses of this lane
+    i32x4_mx B[DPW];
+    uint32_t a0[DPW], a1[DPW];
 #pragma unroll
     for (int j = 0; j < DPW; ++j) {
       const uint32_t mrec = bufb + (uint32_t)(4 * GB + (w * DPW + j) * kMxRec);
       const i32x4_mx ph = *(const lds_i32x4_mx*)(uintptr_t)(mrec + 16 * g4);
       const uint32_t offp = (uint32_t)*(const lds_int_mx*)(uintptr_t)(mrec + 64 + 4 * (8 * g4 + qq));
       // B[k][n] = [phase_k == n]: bytes of ph ^ n that are zero -> 1
-      i32x4_mx B;
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        B[e] = (int)(((~(((uint32_t)ph[e] ^ nn) + 0x7F7F7F7Fu)) >> 7) & 0x01010101u);
+        B[j][e] = (int)(((~(((uint32_t)ph[e] ^ nn) + 0x7F7F7F7Fu)) >> 7) & 0x01010101u);
       const uint32_t o0 = (offp & 0xffffu) + 8u * pp, o1 = (offp >> 16) + 8u * pp;
       const uint32_t col = (uint32_t)((8 * (g4 & 1) + qq) * 16);
-      const uint32_t a0 = bufb + (uint32_t)((g4 >> 1) * GB) + (o0 >> 4) * 256u + col + (o0 & 15u);
-      const uint32_t a1 = bufb + (uint32_t)((2 + (g4 >> 1)) * GB) + (o1 >> 4) * 256u + col + (o1 & 15u);
-#pragma unroll
-      for (int s2 = 0; s2 <= S; ++s2) {
-        const i32x2_mx v0 = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_i32x2_mx*)(uintptr_t)(a0 + 256u * s2));
-        const i32x2_mx v1 = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_i32x2_mx*)(uintptr_t)(a1 + 256u * s2));
-        const i32x4_mx A = (i32x4_mx){v0.x, v0.y, v1.x, v1.y};
-        acc[j][s2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B, acc[j][s2], 0, 0, 0);
-      }
+      a0[j] = bufb + (uint32_t)((g4 >> 1) * GB) + (o0 >> 4) * 256u + col + (o0 & 15u);
+      a1[j] = bufb + (uint32_t)((2 + (g4 >> 1)) * GB) + (o1 >> 4) * 256u + col + (o1 & 15u);
     }
+    // DPW x (S+1) MFMAs in one sequence; the two tr_b8 reads of MFMA i are
+    // issued PF MFMAs ahead into a ring of PF + 1 operand slots (a refill never
+    // targets the slot the current MFMA reads); before MFMA i the wave waits
+    // for all but the younger reads still in flight (LDS reads retire in order)
+    using Seq = MxSeq<S, DPW, 6>;
+    i32x2_mx r0[Seq::NSL], r1[Seq::NSL];
+    Seq::prologue(std::make_integer_sequence<int, 6>{}, r0, r1, a0, a1);
+    Seq::run(std::make_integer_sequence<int, Seq::NM>{}, r0, r1, &acc[0][0], B, a0, a1);
   }
   // ---- combine the phase columns: out[t] = sum_n C[t + n][n] + 128 C
   __syncthreads();
@@ -1117,6 +1204,7 @@ __global__ __launch_bounds__(NW * 64) void k_sweep_mx(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
 }
+#endif  // PDD_SWEEP_DEV
 
 // ------------------------------------------------------------------ variants
 // kind 0: interleaved image + k_sweep_il (dedicated loader waves, NLW);
@@ -1151,18 +1239,22 @@ static const Variant kF32Variants[] = {
     {0, false, 4, 4, 4, 4, 1, 3, 2},   // DB 16, 2 workgroups / CU
     {1, false, 4, 4, 1, 8, 1, 2, 0},   // generic, DB 8
     {1, false, 4, 1, 1, 1, 1, 2, 0}};  // generic, DB 1 (any span that fits 160 KB)
-// 8-bit input: the i8 MFMA kernel (chunk-buffer depth 4, 3, 2 as the
-// windows widen); the u16-eighths VALU kernel (12 compute + 4 loader waves),
-// which grouped 8-bit sweeps use; the float32-image tiling; the generic u16
-// kernel.
+// 8-bit input: u16 eighths (12 compute + 4 loader waves: with half the
+// compute per staged byte the extra loaders pay off), then the float32-image
+// tilings, then the generic u16 kernel.
 static const Variant kU8Variants[] = {
-    {2, true, 16, 0, 2, 8, 64, 4, 0},  // i8 MFMA, DB 16 x 256 times, 4 chunk buffers
-    {2, true, 16, 0, 2, 8, 64, 3, 0},  //   3 buffers (wider windows)
-    {2, true, 16, 0, 2, 8, 64, 2, 0},  //   2 buffers
-    {0, false, 8, 2, 4, 12, 2, 4, 4},  // u16 eighths, DB 48 (grouped 8-bit sweeps)
-    {0, false, 4, 4, 4, 4, 1, 3, 2},   // f32 image of u8 data, DB 16
+    {0, false, 8, 2, 4, 12, 2, 4, 4},  // u16 eighths, DB 48
+    {0, false, 4, 4, 4, 8, 1, 6, 2},   // f32 image of u8 data, DB 32
+    {0, false, 4, 4, 4, 4, 1, 3, 2},   // DB 16
     {1, true, 8, 2, 1, 8, 1, 2, 0},    // generic u16, DB 8
     {1, true, 8, 1, 1, 1, 1, 2, 0}};   // generic u16, DB 1
+
+#ifdef PDD_SWEEP_DEV
+// experimental 8-bit MFMA tilings, tried first when PDD_SWEEP_MX=1
+static const Variant kMxVariants[] = {{2, true, 16, 0, 2, 8, 64, 4, 0},
+                                      {2, true, 16, 0, 2, 8, 64, 3, 0},
+                                      {2, true, 16, 0, 2, 8, 64, 2, 0}};
+#endif
 
 // LDS per workgroup: 16-wave (il) tiles run one per CU, <= 8-wave tiles two
 static int64_t lds_budget(const Variant& v) {
@@ -1187,8 +1279,10 @@ static sweep_il_fn il_kernel_for(const Variant& v) {
   return nullptr;
 }
 
+#ifdef PDD_SWEEP_DEV
 typedef void (*sweep_mx_fn)(const uint8_t*, int64_t, int, const uint8_t*, const uint16_t*,
-                            const uint8_t*, int, float*, int64_t, int, int64_t, int64_t, int, int);
+                            const uint8_t*, int, float*, int64_t, int, int64_t, int64_t, int, int,
+                            int);
 static sweep_mx_fn mx_kernel_for(const Variant& v) {
   if (v.NW == 8 && v.DPW == 2 && v.S == 16) {
     if (v.NBUF == 4) return k_sweep_mx<8, 2, 16, 4>;
@@ -1197,6 +1291,8 @@ static sweep_mx_fn mx_kernel_for(const Variant& v) {
   }
   return nullptr;
 }
+
+#endif
 
 typedef void (*sweep_fn)(const void*, int64_t, int, int64_t, const int*, int, int, const int*,
                          const int*, int, const float*, float*, int64_t, int64_t, int, int, int,
@@ -1267,6 +1363,7 @@ struct pdd_sweep_plan {
 
 using namespace pdd;
 
+#ifdef PDD_SWEEP_DEV
 // Host: tables of the 8-bit MFMA sweep (kind 2) for a [D][C] table; 1 = the
 // variant does not fit this grid (caller tries the next one), < 0 = error.
 static int mx_plan_create(const int32_t* htab, int64_t D, int64_t C, const Variant& v, int vi,
@@ -1281,21 +1378,23 @@ static int mx_plan_create(const int32_t* htab, int64_t D, int64_t C, const Varia
   }
   const int64_t lo = std::min(0, mn), hi = std::max(0, mx);
   if (hi - lo + 16 * S + 256 >= 65536) return 1;  // window starts are u16
-  const int64_t WIN_B = (2 * Cpad + 15) & ~15, ROWS_B = (4 * nchunk + 15) & ~15;
+  const int64_t WIN_B = (2 * (Cpad / 16) + 15) & ~15, ROWS_B = (4 * nchunk + 15) & ~15;
   const int64_t META_B = (int64_t)DB * kMxRec;
-  std::vector<uint16_t> win((size_t)(n_dblk * Cpad), 0);
+  const int64_t ngrp = Cpad / 16;
+  std::vector<uint16_t> win((size_t)(n_dblk * ngrp), 0);
   std::vector<uint8_t> rows((size_t)(n_dblk * nchunk * 4), 0);
   std::vector<uint8_t> meta((size_t)(n_dblk * nchunk * META_B), 0);
   std::vector<int> offk((size_t)Cpad), phk((size_t)Cpad);
   int rows_max = 0;
   for (int64_t b = 0; b < n_dblk; ++b) {
-    // window start of every channel: the block's smallest shift, 16-aligned
-    for (int64_t c = 0; c < Cpad; ++c) {
-      if (c >= C) continue;
+    // window start of every 16-channel group: the smallest shift of the
+    // block over its channels, 16-aligned (one staging window per group)
+    for (int64_t gi = 0; gi < ngrp; ++gi) {
       int bmin = INT32_MAX;
-      for (int64_t d = b * DB; d < (b + 1) * DB; ++d)
-        bmin = std::min(bmin, (int)htab[std::min(d, D - 1) * C + c]);
-      win[(size_t)(b * Cpad + c)] = (uint16_t)((bmin - lo) & ~15);
+      for (int64_t c = gi * 16; c < std::min(C, gi * 16 + 16); ++c)
+        for (int64_t d = b * DB; d < (b + 1) * DB; ++d)
+          bmin = std::min(bmin, (int)htab[std::min(d, D - 1) * C + c]);
+      win[(size_t)(b * ngrp + gi)] = bmin == INT32_MAX ? 0 : (uint16_t)((bmin - lo) & ~15);
     }
     for (int64_t k = 0; k < nchunk; ++k) {
       int rmax[4] = {0, 0, 0, 0};
@@ -1306,7 +1405,7 @@ static int mx_plan_create(const int32_t* htab, int64_t D, int64_t C, const Varia
           int off = 0, ph = 0;
           if (c < C) {
             const int64_t r = (int64_t)htab[d * C + c] - lo;
-            off = (int)((r & ~7) - win[(size_t)(b * Cpad + c)]);
+            off = (int)((r & ~7) - win[(size_t)(b * ngrp + c / 16)]);
             ph = (int)(r & 7);
           }
           offk[(size_t)ch] = off;
@@ -1373,7 +1472,7 @@ static int mx_plan_create(const int32_t* htab, int64_t D, int64_t C, const Varia
   return 0;
 }
 
-// 8-bit MFMA path: time segments whose i8 image R8 ([Cpad][nR8] bytes) fits
+// 8-bit MFMA path: time segments whose i8 image R8 ([Cpad/16][rows][16][16] bytes) fits
 // the scratch budget; each segment is one k_prep8 + one k_sweep_mx.
 static int execute_mx(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t ld, int pad_mode,
                       const float* padvals, float* out, int64_t ld_out, int64_t n_out,
@@ -1398,21 +1497,23 @@ static int execute_mx(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
   for (int64_t t_base = 0; t_base < n_out && rc == 0; t_base += seg) {
     const int64_t cnt = std::min(seg, n_out - t_base);
     const int64_t n_tblk = cdiv(cnt, TT);
-    const int64_t nR8 = (n_tblk * TT + extra + 15) / 16 * 16;
+    const int64_t nrows = cdiv(n_tblk * TT + extra, 16);  // 16-sample rows per group
     const int64_t base = t_base + lo;
     const int fast = ((uintptr_t)x % 16 == 0) && (ld % 16 == 0) && (base % 16 == 0);
-    hipLaunchKernelGGL(k_prep8, dim3((unsigned)cdiv(nR8 / 16, 256), (unsigned)Cpad), dim3(256), 0,
-                       st, (const uint8_t*)x, ld, N, (int)C, base, nR8, pad_mode, padvals, R8, fast);
+    hipLaunchKernelGGL(k_prep8, dim3((unsigned)cdiv(nrows, 64), (unsigned)(Cpad / 16)), dim3(256),
+                       0, st, (const uint8_t*)x, ld, N, (int)C, base, nrows, pad_mode, padvals, R8,
+                       fast);
     if (hipGetLastError() != hipSuccess) { rc = -3; break; }
-    const int64_t blocks = n_tblk * p->n_dblk;
+    const int64_t blocks = n_tblk * cdiv(p->n_dblk, 8) * 8;  // see k_sweep_mx tile order
     if (blocks >= (1ll << 31)) { rc = -1; break; }
     pdd_sweep_plan* pm = const_cast<pdd_sweep_plan*>(p);
     const bool bracket = p->timing && p->timed < pdd_sweep_plan::kEvPairs;
     if (p->timing && !bracket) pm->dropped++;
     if (bracket) (void)hipEventRecord(p->ev[2 * p->timed], st);
-    hipLaunchKernelGGL(kf, dim3((unsigned)blocks), dim3(p->v.NW * 64), p->lds_bytes, st, R8, nR8,
+    hipLaunchKernelGGL(kf, dim3((unsigned)blocks), dim3(p->v.NW * 64), p->lds_bytes, st, R8, nrows,
                        p->nchunk, p->d_meta, p->d_win, p->d_rows, p->rows_max, out, ld_out,
-                       (int)p->D, t_base, t_base + cnt, (int)p->n_dblk, (int)(128 * C));
+                       (int)p->D, t_base, t_base + cnt, (int)p->n_dblk, (int)(128 * C),
+                       debug_flags());
     if (hipGetLastError() != hipSuccess) rc = -3;
     if (bracket) {
       (void)hipEventRecord(p->ev[2 * p->timed + 1], st);
@@ -1424,6 +1525,7 @@ static int execute_mx(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
   if (rc == -3) set_error("pdd_sweep_execute: kernel launch failed");
   return rc;
 }
+#endif  // PDD_SWEEP_DEV
 
 // Interleaved path: the output is produced in time segments whose
 // interleaved copy R fits a scratch budget (stream-ordered allocation, freed
@@ -1510,15 +1612,17 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
   const int ncand = dtype == PDD_U8 ? (int)(sizeof(kU8Variants) / sizeof(Variant))
                                     : (int)(sizeof(kF32Variants) / sizeof(Variant));
 
+#ifdef PDD_SWEEP_DEV
+  if (dtype == PDD_U8 && n_grp == 1 && getenv("PDD_SWEEP_MX")) {
+    for (int mi = 0; mi < 3; ++mi) {
+      const int r = mx_plan_create(host_table, D, C, kMxVariants[mi], 100 + mi, plan_out);
+      if (r <= 0) return r;
+    }
+  }
+#endif
   const int fv = forced_variant();
   for (int vi = (fv >= 0 && fv < ncand) ? fv : 0; vi < ncand; ++vi) {
     const Variant v = cands[vi];
-    if (v.kind == 2) {
-      if (n_grp > 1) continue;  // the MFMA kernel sweeps one group
-      const int r = mx_plan_create(host_table, D, C, v, vi, plan_out);
-      if (r <= 0) return r;
-      continue;
-    }
     const bool il = v.kind == 0;
     if (n_grp > 1 && !il) continue;  // only the interleaved kernel sweeps groups
     const int64_t DB = v.DB();
@@ -1649,7 +1753,9 @@ int pdd_sweep_execute(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
   PDD_REQUIRE(pad_mode == PDD_PAD_ROTATE || (pad_mode == PDD_PAD_VALUE && padvals),
               "pdd_sweep_execute: bad pad mode %d", pad_mode);
   if (n_out == 0) return 0;
+#ifdef PDD_SWEEP_DEV
   if (p->v.kind == 2) return execute_mx(p, x, N, ld, pad_mode, padvals, out, ld_out, n_out, stream);
+#endif
   if (p->v.kind == 0) return execute_il(p, x, N, ld, pad_mode, padvals, out, ld_out, n_out, 0, 1, stream);
   // every staged index must stay inside int64 / the LDS image: the shifts are
   // bounded by the plan, the samples by N + n_out.

@@ -375,10 +375,9 @@ def test_deepcopy_independent(S):
 # Every tiling the plan can choose, reached by a grid whose per-trial-block
 # shift span forces it (pdd_sweep.hip kF32Variants / kU8Variants, best first),
 # each checked against the oracle: (dDM, expected variant index).  Span ~
-# (DB - 1) * 14.5 * dDM bins at the bottom channel.  u8 index 3 (the u16
-# VALU kernel) is only chosen for grouped 8-bit sweeps: test below.
+# (DB - 1) * 14.5 * dDM bins at the bottom channel.
 LADDER = {"f32": [(0.5, 0), (2.0, 1), (4.5, 2), (12.0, 3), (40.0, 4)],
-          "u8": [(0.5, 0), (1.6, 1), (3.0, 2), (5.0, 4), (12.0, 5), (40.0, 6)]}
+          "u8": [(0.5, 0), (2.0, 1), (4.5, 2), (12.0, 3), (40.0, 4)]}
 
 
 @pytest.mark.gpu
@@ -408,7 +407,7 @@ def test_sweep_variant_ladder(gpu, dtype):
 @pytest.mark.gpu
 @pytest.mark.parametrize("pad", [0, 7, "rotate"])
 def test_grouped_u8_sweep(gpu, pad):
-    """Grouped 8-bit sweep (u16-eighths VALU kernel, kU8Variants[3]): two
+    """Grouped 8-bit sweep (u16-eighths VALU kernel, kU8Variants[0]): two
     channel groups with their own tables, against per-group oracle planes."""
     import torch
     from pypulsar_amd import _lib
