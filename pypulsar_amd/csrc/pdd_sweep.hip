@@ -550,17 +550,19 @@ __device__ __forceinline__ int stage_il_dma(uint32_t lds_dst, const float4* src,
 // reads and returns out of order, so every counted LDS wait became
 // lgkmcnt(0): f32 43 -> 62 ms.)
 // Metadata: mt[dblk][c][ROW], ROW = DB + 4: the tile's DB shifts at channel c
-// relative to their minimum bmin, then {bmin, span, 0, 0}.  Every loader wave
-// DMAs the rows of chunk k into its own ring (slot k % MR) MA = NBUF chunks
-// (MA = 2(NBUF-1)) ahead, so they have landed (its own counted vmcnt) before
-// it reads the window bounds; the compute waves read the shifts from loader
-// 0's ring once the
-// chunk's barrier has passed.
+// relative to their minimum bmin, then {bmin, span, 0, 0}.  Loader 0 DMAs
+// the rows of chunk j into ONE shared ring (slot j % MR) MA = 2(NBUF-1)
+// chunks ahead, before the samples of chunk j - MA + NBUF - 1; its counted
+// vmcnt before barrier k therefore also retires the rows of chunk
+// k + NBUF - 1, which every loader reads after barrier k to issue that
+// chunk's samples, and the compute waves read the shifts of chunk k after
+// the same barrier.  (One ring instead of one per loader: the LDS it frees
+// buys wider chunks -- fewer barriers per channel.)
 __host__ __device__ constexpr int il_ma(int nbuf) { return 2 * nbuf - 2; }
 __host__ __device__ constexpr int il_mr(int nbuf) { return nbuf <= 4 ? 8 : (nbuf <= 8 ? 16 : 32); }
 __host__ __device__ constexpr int il_slot(int cc, int db) { return (cc * (db + 4) + 63) / 64 * 64; }
-__host__ __device__ constexpr int il_meta_bytes(int nlw, int nbuf, int cc, int db) {
-  return nlw * il_mr(nbuf) * il_slot(cc, db) * 4;
+__host__ __device__ constexpr int il_meta_bytes(int nbuf, int cc, int db) {
+  return il_mr(nbuf) * il_slot(cc, db) * 4;
 }
 
 // Tile order of k_sweep_il.  Blocks b and b+8 share an XCD (and its L2).
@@ -633,7 +635,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   extern __shared__ __attribute__((aligned(16))) float smf[];
   uint4* img = reinterpret_cast<uint4*>(smf);
   const int buf_e = CC * stride;
-  int* metar = reinterpret_cast<int*>(img + NBUF * buf_e);  // [NLW][MR][SLOT]
+  int* metar = reinterpret_cast<int*>(img + NBUF * buf_e);  // [MR][SLOT]
 
   const int per_grp = n_tblk * n_dblk;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -662,9 +664,9 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     if (!(dbg & 8)) __builtin_amdgcn_s_setprio(3);
     const int lw = w - NCW;
     const uint32_t img_lds = lds_addr_of(img);
-    int* ring = metar + lw * MR * SLOT;
+    int* ring = metar;  // the shared ring (loader 0 fills it)
     auto issue_meta = [&](int k) -> int {
-      if (k >= nchunk) return 0;
+      if (lw != 0 || k >= nchunk) return 0;
       const int n_int = min(CC, C - k * CC) * ROW;
       int n = 0;
 #pragma unroll
@@ -1234,16 +1236,25 @@ struct Variant {
 // Every entry is reached by a named test (tests/test_gpu_parity.py
 // test_sweep_variant_ladder).
 static const Variant kF32Variants[] = {
-    {0, false, 4, 4, 4, 14, 2, 4, 2},  // DB 56, 1 workgroup / CU
+    {0, false, 4, 4, 4, 14, 8, 3, 2},  // DB 56, 8-channel chunks (fewest barriers)
+    {0, false, 4, 4, 4, 14, 4, 4, 2},  //   4-channel chunks
+    {0, false, 4, 4, 4, 14, 4, 3, 2},  //   4-channel chunks, 3 buffers
+    {0, false, 4, 4, 4, 14, 3, 3, 2},  //   3-channel chunks
+    {0, false, 4, 4, 4, 14, 2, 4, 2},  //   2-channel chunks (configs[1]: wide windows)
     {0, false, 4, 4, 4, 8, 1, 6, 2},   // DB 32
     {0, false, 4, 4, 4, 4, 1, 3, 2},   // DB 16, 2 workgroups / CU
     {1, false, 4, 4, 1, 8, 1, 2, 0},   // generic, DB 8
     {1, false, 4, 1, 1, 1, 1, 2, 0}};  // generic, DB 1 (any span that fits 160 KB)
 // 8-bit input: u16 eighths (12 compute + 4 loader waves: with half the
-// compute per staged byte the extra loaders pay off), then the float32-image
-// tilings, then the generic u16 kernel.
+// compute per staged byte the extra loaders pay off) in chunks as wide as the
+// LDS allows (measured, BASELINE configs[3]: 2 / 3 / 4 / 8 channels per chunk
+// = 376 / 333 / 315 / 298 ms per launch), then the float32-image tilings,
+// then the generic u16 kernel.
 static const Variant kU8Variants[] = {
-    {0, false, 8, 2, 4, 12, 2, 4, 4},  // u16 eighths, DB 48
+    {0, false, 8, 2, 4, 12, 8, 3, 4},  // u16 eighths, DB 48, 8-channel chunks
+    {0, false, 8, 2, 4, 12, 4, 4, 4},  //   4-channel chunks
+    {0, false, 8, 2, 4, 12, 4, 3, 4},  //   4-channel chunks, 3 buffers
+    {0, false, 8, 2, 4, 12, 3, 3, 4},  //   3-channel chunks (configs[1])
     {0, false, 4, 4, 4, 8, 1, 6, 2},   // f32 image of u8 data, DB 32
     {0, false, 4, 4, 4, 4, 1, 3, 2},   // DB 16
     {1, true, 8, 2, 1, 8, 1, 2, 0},    // generic u16, DB 8
@@ -1270,8 +1281,16 @@ static sweep_il_fn il_kernel_for(const Variant& v) {
   if (v.S == 4 && v.NW == NCW_ && v.NLW == NLW_ && v.CC == CC_ && v.NBUF == NB_ && v.G == 4 && \
       v.DPW == 4)                                                                               \
     return k_sweep_il<4, 4, NCW_, NLW_, CC_, NB_>;
-  if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.CC == 2 && v.NBUF == 4 && v.G == 2 && v.DPW == 4)
-    return k_sweep_il<2, 4, 12, 4, 2, 4, true>;
+  if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.DPW == 4) {
+    if (v.CC == 8 && v.NBUF == 3) return k_sweep_il<2, 4, 12, 4, 8, 3, true>;
+    if (v.CC == 4 && v.NBUF == 4) return k_sweep_il<2, 4, 12, 4, 4, 4, true>;
+    if (v.CC == 4 && v.NBUF == 3) return k_sweep_il<2, 4, 12, 4, 4, 3, true>;
+    if (v.CC == 3 && v.NBUF == 3) return k_sweep_il<2, 4, 12, 4, 3, 3, true>;
+  }
+  IL(14, 2, 8, 3)
+  IL(14, 2, 4, 4)
+  IL(14, 2, 4, 3)
+  IL(14, 2, 3, 3)
   IL(14, 2, 2, 4)
   IL(8, 2, 1, 6)
   IL(4, 2, 1, 3)
@@ -1613,7 +1632,7 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
                                     : (int)(sizeof(kF32Variants) / sizeof(Variant));
 
 #ifdef PDD_SWEEP_DEV
-  if (dtype == PDD_U8 && n_grp == 1 && getenv("PDD_SWEEP_MX")) {
+  if (dtype == PDD_U8 && n_grp == 1 && getenv("PDD_SWEEP_MX") && atoi(getenv("PDD_SWEEP_MX"))) {
     for (int mi = 0; mi < 3; ++mi) {
       const int r = mx_plan_create(host_table, D, C, kMxVariants[mi], 100 + mi, plan_out);
       if (r <= 0) return r;
@@ -1679,7 +1698,7 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
     const int64_t per_chan = v.NBUF * v.chan_bytes(stride);
     const bool last = (vi == ncand - 1);
     // linear kernel: metadata rings (NBUF x 64 ints x 2) after the buffers
-    const int64_t need = per_chan * v.CC + (il ? il_meta_bytes(v.NLW, v.NBUF, v.CC, v.DB()) : 0);
+    const int64_t need = per_chan * v.CC + (il ? il_meta_bytes(v.NBUF, v.CC, v.DB()) : 0);
     if (il && (int64_t)max_span + 64 * v.G > (int64_t)1 << 20) continue;  // windows too wide
     if (need > lds_budget(v) && !(last && need <= kLdsMax)) {
       if (last) {

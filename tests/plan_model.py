@@ -1,0 +1,48 @@
+"""Model of pdd_sweep_plan_create's tiling choice (pdd_sweep.hip
+kF32Variants / kU8Variants, lds_budget, il_meta_bytes): test infrastructure
+that picks one DM grid per candidate for tests/test_gpu_parity.py
+test_sweep_variant_ladder, which also asserts the library chose the same."""
+import numpy as np
+
+# (kind, u8, S, G, DPW, NW, CC, NBUF, NLW), as in pdd_sweep.hip
+F32 = [(0, 0, 4, 4, 4, 14, 8, 3, 2), (0, 0, 4, 4, 4, 14, 4, 4, 2), (0, 0, 4, 4, 4, 14, 4, 3, 2),
+       (0, 0, 4, 4, 4, 14, 3, 3, 2), (0, 0, 4, 4, 4, 14, 2, 4, 2), (0, 0, 4, 4, 4, 8, 1, 6, 2),
+       (0, 0, 4, 4, 4, 4, 1, 3, 2), (1, 0, 4, 4, 1, 8, 1, 2, 0), (1, 0, 4, 1, 1, 1, 1, 2, 0)]
+U8 = [(0, 0, 8, 2, 4, 12, 8, 3, 4), (0, 0, 8, 2, 4, 12, 4, 4, 4), (0, 0, 8, 2, 4, 12, 4, 3, 4),
+      (0, 0, 8, 2, 4, 12, 3, 3, 4), (0, 0, 4, 4, 4, 8, 1, 6, 2), (0, 0, 4, 4, 4, 4, 1, 3, 2),
+      (1, 1, 8, 2, 1, 8, 1, 2, 0), (1, 1, 8, 1, 1, 1, 1, 2, 0)]
+
+
+def _mr(nbuf):
+    return 8 if nbuf <= 4 else (16 if nbuf <= 8 else 32)
+
+
+def _slot(cc, db):
+    return (cc * (db + 4) + 63) // 64 * 64
+
+
+def choose(table, dtype):
+    """Index of the candidate the plan takes for an int [D, C] table."""
+    cands = U8 if dtype == "u8" else F32
+    D, C = table.shape
+    for vi, (kind, u8, S, G, DPW, NW, CC, NBUF, NLW) in enumerate(cands):
+        DB = NW * DPW
+        nb = -(-D // DB)
+        t = table[np.minimum(np.arange(nb * DB), D - 1)].reshape(nb, DB, C)
+        span = int((t.max(axis=1) - t.min(axis=1)).max())
+        if kind == 0:
+            stride = (64 * G + span + 63) // 64 * 64
+            elem = 16
+            need = NBUF * stride * elem * CC + _mr(NBUF) * _slot(CC, DB) * 4
+            budget = 78 * 1024 if (NW + NLW) * 2 <= 16 else 158 * 1024
+            if span + 64 * G > (1 << 20):
+                continue
+        else:
+            stride = (64 * G + span + 15) // 16 * 16
+            elem = 2 * S if u8 else 4 * S
+            need = NBUF * stride * elem * CC
+            budget = 150 * 1024 if NW >= 16 else 76 * 1024
+        last = vi == len(cands) - 1
+        if need <= budget or (last and need <= 160 * 1024):
+            return vi
+    return None

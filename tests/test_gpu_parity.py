@@ -374,17 +374,18 @@ def test_deepcopy_independent(S):
 
 # Every tiling the plan can choose, reached by a grid whose per-trial-block
 # shift span forces it (pdd_sweep.hip kF32Variants / kU8Variants, best first),
-# each checked against the oracle: (dDM, expected variant index).  Span ~
-# (DB - 1) * 14.5 * dDM bins at the bottom channel.
-LADDER = {"f32": [(0.5, 0), (2.0, 1), (4.5, 2), (12.0, 3), (40.0, 4)],
-          "u8": [(0.5, 0), (2.0, 1), (4.5, 2), (12.0, 3), (40.0, 4)]}
+# each checked against the oracle.  The dDM of each rung comes from the
+# plan-selection model tests/plan_model.py (asserted equal to the library's
+# choice): rung i selects candidate i.
+LADDER = {"f32": [0.07, 0.25, 0.55, 0.85, 1.1, 2.0, 4.5, 12.0, 40.0],
+          "u8": [0.2, 0.55, 0.85, 1.2, 2.0, 4.5, 12.0, 40.0]}
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["f32", "u8"])
 def test_sweep_variant_ladder(gpu, dtype):
     import torch
-    from oracle import spectra_oracle as orc
+    import plan_model
     from pypulsar_amd.sweep import DMSweep
     C, N, D = 32, 49152, 64
     freqs = band(C)
@@ -393,13 +394,15 @@ def test_sweep_variant_ladder(gpu, dtype):
     if dtype == "f32":
         xd = xd.float()
     code = 1 if dtype == "u8" else 0
-    for ddm, want_v in LADDER[dtype]:
+    for want_v, ddm in enumerate(LADDER[dtype]):
         dms = np.arange(D) * ddm
+        tab = orc.sweep_table(dms, freqs, DT)
+        assert plan_model.choose(tab, dtype) == want_v
         sw = DMSweep(dms, freqs, DT, dtype=dtype)
         v = sw.info(code)["variant"]
         assert v == want_v, "dDM %g chose variant %d, expected %d" % (ddm, v, want_v)
         plane = sw(xd).cpu().numpy().astype(np.float64)
-        want = orc.sweep_plane(x.astype(np.float64), orc.sweep_table(dms, freqs, DT))
+        want = orc.sweep_plane(x.astype(np.float64), tab)
         np.testing.assert_array_equal(plane, want, err_msg="dDM %g (variant %d)" % (ddm, v))
         sw.close()
 

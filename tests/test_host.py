@@ -160,3 +160,31 @@ def test_config2_two_stage_tables_match_reference(grids):
     np.testing.assert_array_equal(ctr, g["cfg2_ctr"])
     t2 = delays.sweep_table(np.concatenate([c[1] for c in calls]), ctr, dt)
     _check_rows(g, "cfg2s2", t2)
+
+
+def test_plan_model_ladder_covers_every_tiling():
+    """The ladder grids of test_sweep_variant_ladder select every candidate
+    tiling (pdd_sweep.hip), in order, under the plan-selection model."""
+    import plan_model
+    from oracle import spectra_oracle as orc
+    from test_gpu_parity import LADDER
+    freqs = band(32)
+    for dtype, cands in (("f32", plan_model.F32), ("u8", plan_model.U8)):
+        got = [plan_model.choose(orc.sweep_table(np.arange(64) * d, freqs, DT), dtype)
+               for d in LADDER[dtype]]
+        assert got == list(range(len(cands))), (dtype, got)
+
+
+def test_plan_model_matches_kernel_tables():
+    """tests/plan_model.py restates the candidate tables of pdd_sweep.hip."""
+    import re
+    import plan_model
+    src = open(os.path.join(os.path.dirname(GOLDEN), "..", "pypulsar_amd", "csrc",
+                            "pdd_sweep.hip")).read()
+    for name, model in (("kF32Variants", plan_model.F32), ("kU8Variants", plan_model.U8)):
+        body = src[src.index("static const Variant %s[] = {" % name):]
+        body = body[:body.index("};")]
+        rows = [tuple(int(v) if v not in ("true", "false") else int(v == "true")
+                      for v in (x.strip() for x in m.split(",")))
+                for m in re.findall(r"\{([-\w, ]+)\}", body)]
+        assert rows == model, name
