@@ -151,6 +151,19 @@ int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int d
 int pdd_sweep_execute(const pdd_sweep_plan* plan, const void* x, int64_t N, int64_t ld,
                       int pad_mode, const float* padvals, float* out, int64_t ld_out,
                       int64_t n_out, void* stream);
+/* The same with two more input layouts/offsets (DM-sharded sweeps):
+ *   piece == 0: x is channel-major [C][ld];
+ *   piece == P > 0 (a power of two): x is [ceil(N/P)][C][P] -- the block an
+ *     all-gather of per-rank channel-major time slices of P samples produces
+ *     (sample s of channel c at x[(s/P)*C*P + c*P + s%P]);
+ *   x_off: plane column t sums input samples t + x_off + table[d][c] (a column
+ *     range [x_off, x_off + n_out) of the full sweep); pads apply outside
+ *     [0, N) of x.
+ * Offsets and pieces need the interleaved tilings (every grid whose shift
+ * span per trial block fits the LDS); sparser grids return an error. */
+int pdd_sweep_execute_ex(const pdd_sweep_plan* plan, const void* x, int64_t N, int64_t ld,
+                         int64_t piece, int64_t x_off, int pad_mode, const float* padvals,
+                         float* out, int64_t ld_out, int64_t n_out, void* stream);
 /* Grouped sweep: n_grp independent channel groups of C channels each
  * (channels g*C .. g*C+C-1 of the input), every group with its own [D][C]
  * table: host_table is [n_grp][D][C].  One launch replaces n_grp sweeps --

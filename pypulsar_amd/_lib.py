@@ -33,6 +33,7 @@ EXPORTS = (
     "pdd_smooth", "pdd_zdm_downsample", "pdd_sweep_set_timing", "pdd_sweep_kernel_ms",
     "pdd_sweep_plan_create_grouped", "pdd_sweep_execute_grouped", "pdd_sp_chunk_stats",
     "pdd_sp_search", "pdd_psrfits_subints", "pdd_downsample_u8", "pdd_sweep_timing_read",
+    "pdd_sweep_execute_ex",
 )
 
 
@@ -62,6 +63,8 @@ _SIGS = {
     "pdd_zero_dm": ([_vp, _int, _i64, _i64, _i64, _int, _vp, _i64, _vp], _int),
     "pdd_sweep_plan_create": ([_vp, _i64, _i64, _int, ctypes.POINTER(_vp)], _int),
     "pdd_sweep_execute": ([_vp, _vp, _i64, _i64, _int, _vp, _vp, _i64, _i64, _vp], _int),
+    "pdd_sweep_execute_ex": ([_vp, _vp, _i64, _i64, _i64, _i64, _int, _vp, _vp, _i64, _i64, _vp],
+                             _int),
     "pdd_sweep_plan_info": ([_vp, _vp], _int),
     "pdd_sweep_plan_destroy": ([_vp], _int),
     "pdd_global_stats": ([_vp, _i64, _i64, _i64, _vp, _vp], _int),

@@ -461,14 +461,28 @@ __device__ __forceinline__ void dma_ints(int* lds_dst, const int* src, int n, in
 // Each thread writes kIlPer elements 256 apart, issuing all their loads
 // before any store (memory-level parallelism for the strided quarter reads).
 constexpr int kIlPer = 4;
+// Input layouts of the pre-pass: channel-major rows (x[c * ld + s]) or the
+// "pieces" layout an all-gather of channel-major time slices produces,
+// x[(s / P) * C * P + c * P + s % P] (P = piece, a power of two; C = all
+// channels of the plan).
+struct InLayout {
+  int64_t ld;      // channel-major row stride (piece == 0)
+  int64_t piece;   // P, 0 = channel-major
+  int psh;         // log2(P)
+  int64_t pstride; // C * P
+  __device__ __forceinline__ int64_t at(int c, int64_t s) const {
+    return piece ? (s >> psh) * pstride + (int64_t)c * piece + (s & (piece - 1))
+                 : (int64_t)c * ld + s;
+  }
+};
+
 template <typename InT>
-__global__ __launch_bounds__(256) void k_interleave(const InT* __restrict__ x, int64_t ld, int64_t N,
+__global__ __launch_bounds__(256) void k_interleave(const InT* __restrict__ x, InLayout lay, int64_t N,
                                                     int64_t base, int64_t Qs, int64_t nR,
                                                     int pad_mode, const float* __restrict__ padvals,
                                                     float4* __restrict__ R) {
   const int c = blockIdx.y;
   const int64_t j0 = (int64_t)blockIdx.x * (256 * kIlPer) + threadIdx.x;
-  const InT* row = x + (int64_t)c * ld;
   const float pv = (pad_mode == PDD_PAD_VALUE) ? padvals[c] : 0.f;
   float v[kIlPer][4];
 #pragma unroll
@@ -476,8 +490,8 @@ __global__ __launch_bounds__(256) void k_interleave(const InT* __restrict__ x, i
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int64_t s = base + j0 + i * 256 + k * Qs;
-      if (s >= 0 && s < N) v[i][k] = (float)row[s];
-      else if (pad_mode == PDD_PAD_ROTATE) v[i][k] = (float)row[wrap_mod(s, N)];
+      if (s >= 0 && s < N) v[i][k] = (float)x[lay.at(c, s)];
+      else if (pad_mode == PDD_PAD_ROTATE) v[i][k] = (float)x[lay.at(c, wrap_mod(s, N))];
       else v[i][k] = pv;
     }
 #pragma unroll
@@ -490,14 +504,13 @@ __global__ __launch_bounds__(256) void k_interleave(const InT* __restrict__ x, i
 // u16 eighths for 8-bit data: R[c][j] = 8 samples X(c, b + j + k*Qs), k < 8,
 // as packed u16 pairs (word h = sample 2h | sample 2h+1 << 16); pads (integer
 // values 0..255, checked by the caller) and rotation baked in as for float32.
-__global__ __launch_bounds__(256) void k_interleave_u16(const uint8_t* __restrict__ x, int64_t ld,
+__global__ __launch_bounds__(256) void k_interleave_u16(const uint8_t* __restrict__ x, InLayout lay,
                                                         int64_t N, int64_t base, int64_t Qs,
                                                         int64_t nR, int pad_mode,
                                                         const float* __restrict__ padvals,
                                                         uint4* __restrict__ R) {
   const int c = blockIdx.y;
   const int64_t j0 = (int64_t)blockIdx.x * (256 * kIlPer) + threadIdx.x;
-  const uint8_t* row = x + (int64_t)c * ld;
   const uint32_t pv = (pad_mode == PDD_PAD_VALUE) ? (uint32_t)padvals[c] : 0u;
   uint32_t v[kIlPer][8];
 #pragma unroll
@@ -505,8 +518,8 @@ __global__ __launch_bounds__(256) void k_interleave_u16(const uint8_t* __restric
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int64_t s = base + j0 + i * 256 + k * Qs;
-      if (s >= 0 && s < N) v[i][k] = row[s];
-      else if (pad_mode == PDD_PAD_ROTATE) v[i][k] = row[wrap_mod(s, N)];
+      if (s >= 0 && s < N) v[i][k] = x[lay.at(c, s)];
+      else if (pad_mode == PDD_PAD_ROTATE) v[i][k] = x[lay.at(c, wrap_mod(s, N))];
       else v[i][k] = pv;
     }
 #pragma unroll
@@ -1549,9 +1562,9 @@ static int execute_mx(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
 // Interleaved path: the output is produced in time segments whose
 // interleaved copy R fits a scratch budget (stream-ordered allocation, freed
 // after the segment loop); each segment is one k_interleave + one k_sweep_il.
-static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t ld, int pad_mode,
-                      const float* padvals, float* out, int64_t ld_out, int64_t n_out,
-                      int64_t row_g, int64_t row_d, void* stream) {
+static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayout lay,
+                      int64_t x_off, int pad_mode, const float* padvals, float* out,
+                      int64_t ld_out, int64_t n_out, int64_t row_g, int64_t row_d, void* stream) {
   const int Tq = 64 * p->v.G;
   const int SP = p->v.S;  // samples per element: 4 (float32 quarters) or 8 (u16 eighths)
   const bool u16 = (SP == 8);
@@ -1581,14 +1594,14 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
     const int64_t nR = Qs + (hi - lo) + 64;
     dim3 g1((unsigned)cdiv(nR, 256 * kIlPer), (unsigned)C);
     if (u16)
-      hipLaunchKernelGGL(k_interleave_u16, g1, dim3(256), 0, st, (const uint8_t*)x, ld, N,
-                         t_base + lo, Qs, nR, pad_mode, padvals, (uint4*)R);
+      hipLaunchKernelGGL(k_interleave_u16, g1, dim3(256), 0, st, (const uint8_t*)x, lay, N,
+                         t_base + lo + x_off, Qs, nR, pad_mode, padvals, (uint4*)R);
     else if (p->dtype == PDD_U8)
-      hipLaunchKernelGGL(k_interleave<uint8_t>, g1, dim3(256), 0, st, (const uint8_t*)x, ld, N,
-                         t_base + lo, Qs, nR, pad_mode, padvals, R);
+      hipLaunchKernelGGL(k_interleave<uint8_t>, g1, dim3(256), 0, st, (const uint8_t*)x, lay, N,
+                         t_base + lo + x_off, Qs, nR, pad_mode, padvals, R);
     else
-      hipLaunchKernelGGL(k_interleave<float>, g1, dim3(256), 0, st, (const float*)x, ld, N,
-                         t_base + lo, Qs, nR, pad_mode, padvals, R);
+      hipLaunchKernelGGL(k_interleave<float>, g1, dim3(256), 0, st, (const float*)x, lay, N,
+                         t_base + lo + x_off, Qs, nR, pad_mode, padvals, R);
     if (hipGetLastError() != hipSuccess) { rc = -3; break; }
     const int64_t n_tblk = Qs / Tq;
     const int64_t blocks = n_tblk * p->n_dblk * p->n_grp;
@@ -1767,15 +1780,35 @@ int pdd_sweep_plan_info(const pdd_sweep_plan* p, int64_t* info) {
 int pdd_sweep_execute(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t ld, int pad_mode,
                       const float* padvals, float* out, int64_t ld_out, int64_t n_out,
                       void* stream) {
+  return pdd_sweep_execute_ex(p, x, N, ld, 0, 0, pad_mode, padvals, out, ld_out, n_out, stream);
+}
+
+int pdd_sweep_execute_ex(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t ld,
+                         int64_t piece, int64_t x_off, int pad_mode, const float* padvals,
+                         float* out, int64_t ld_out, int64_t n_out, void* stream) {
   PDD_REQUIRE(p && x && out, "pdd_sweep_execute: null pointer");
-  PDD_REQUIRE(N > 0 && ld >= N && n_out >= 0 && ld_out >= n_out, "pdd_sweep_execute: bad shape");
+  PDD_REQUIRE(N > 0 && n_out >= 0 && ld_out >= n_out && x_off >= 0, "pdd_sweep_execute: bad shape");
+  PDD_REQUIRE(piece > 0 || ld >= N, "pdd_sweep_execute: row stride %lld < N", (long long)ld);
+  PDD_REQUIRE(piece == 0 || (piece & (piece - 1)) == 0, "pdd_sweep_execute: piece must be 2^k");
   PDD_REQUIRE(pad_mode == PDD_PAD_ROTATE || (pad_mode == PDD_PAD_VALUE && padvals),
               "pdd_sweep_execute: bad pad mode %d", pad_mode);
   if (n_out == 0) return 0;
+  InLayout lay{ld, piece, 0, 0};
+  if (piece) {
+    while ((1ll << lay.psh) < piece) ++lay.psh;
+    lay.pstride = p->C * p->n_grp * piece;
+  }
 #ifdef PDD_SWEEP_DEV
-  if (p->v.kind == 2) return execute_mx(p, x, N, ld, pad_mode, padvals, out, ld_out, n_out, stream);
+  if (p->v.kind == 2) {
+    PDD_REQUIRE(piece == 0 && x_off == 0, "pdd_sweep_execute: MFMA path reads channel-major input");
+    return execute_mx(p, x, N, ld, pad_mode, padvals, out, ld_out, n_out, stream);
+  }
 #endif
-  if (p->v.kind == 0) return execute_il(p, x, N, ld, pad_mode, padvals, out, ld_out, n_out, 0, 1, stream);
+  if (p->v.kind == 0)
+    return execute_il(p, x, N, lay, x_off, pad_mode, padvals, out, ld_out, n_out, 0, 1, stream);
+  PDD_REQUIRE(piece == 0 && x_off == 0,
+              "pdd_sweep_execute: the generic (sparse-grid) kernel reads channel-major input "
+              "at offset 0 only");
   // every staged index must stay inside int64 / the LDS image: the shifts are
   // bounded by the plan, the samples by N + n_out.
   const int64_t n_tblk = cdiv(n_out, p->v.TB());
@@ -1801,7 +1834,8 @@ int pdd_sweep_execute_grouped(const pdd_sweep_plan* p, const void* x, int64_t N,
   PDD_REQUIRE(pad_mode == PDD_PAD_ROTATE || (pad_mode == PDD_PAD_VALUE && padvals),
               "pdd_sweep_execute_grouped: bad pad mode %d", pad_mode);
   if (n_out == 0) return 0;
-  return execute_il(p, x, N, ld, pad_mode, padvals, out, ld_out, n_out, row_g, row_d, stream);
+  return execute_il(p, x, N, InLayout{ld, 0, 0, 0}, 0, pad_mode, padvals, out, ld_out, n_out, row_g,
+                    row_d, stream);
 }
 
 int pdd_sweep_set_timing(pdd_sweep_plan* p, int on) {

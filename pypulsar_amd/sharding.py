@@ -126,32 +126,37 @@ class DMShardedSweep(object):
 
     Input layout (file order, time-major): the block is cut into ``n_batches``
     time batches of T = N / n_batches spectra; rank r holds, for each batch k,
-    spectra [k*T + r*T/W, k*T + (r+1)*T/W) -- ``part`` is [n_batches, T/W, C]
-    (its own 1/W H2D slice of every batch).
+    spectra [k*T + r*P, k*T + (r+1)*P), P = T/W -- ``part`` is
+    [n_batches, P, C] (its own 1/W H2D slice of every batch).
 
-    One ``__call__`` (a bench step):
-        issue all-gather of batch 0
+    One ``__call__`` (a bench step), when P is a power of two ("pieces"):
         for k in 0..n_batches-1:
-            wait batch k; issue all-gather of batch k+1  (overlaps the sweep below)
-            corner-turn batch k -> x[:, kT:(k+1)T]        (pdd_corner_turn)
-            sweep plane columns [col_edges[k], col_edges[k+1]) of this rank's
-              DM slice from x[:, col_edges[k] : col_edges[k+1] + max_bin]
-            (gather=True: send this batch's rows to ``dst``, async, which
-             receives them into its full [D, cols_k] batch plane)
-    Column block k needs input up to col_edges[k+1] + max_bin <= (k+1)T, so it
-    is computable as soon as batch k has arrived.  All delays are >= 0 here
-    (cur_dm = 0, dms >= 0, reference = the highest frequency), so no pad value
-    is ever read and a view of x is exactly the reference's input.
+            corner-turn this rank's slice of batch k -> [C, P]   (pdd_corner_turn,
+              1/W of the block per rank, not the whole block)
+            all-gather batch k's slices (async RCCL) -> pieces [kW, (k+1)W)
+              of the [N/P][C][P] block (issued before batch k-1's sweep, so
+              the exchange of batch k overlaps the sweep of batch k-1)
+            sweep plane columns of batch k-1 straight from the pieces
+              (pdd_sweep_execute_ex: pieces layout + column offset)
+        (gather=True: each batch's rows are also sent to ``dst``, async,
+         which receives them into its full [D, cols_k] batch plane)
+    Otherwise the slices are all-gathered time-major and every rank
+    corner-turns the whole batch (the same pipeline).  Column block k needs
+    input up to col_edges[k+1] + max_bin <= (k+1)T.  All delays are >= 0
+    (cur_dm = 0, dms >= 0, reference = the highest frequency), so no pad is
+    ever read.
 
     Plans (delay table, sweep plan, buffers) are built once in __init__;
     ``work`` (per-trial weights, e.g. ``trial_work``) balances the DM slices.
-    ``to_cm(src_tc, dst_cm_view)`` and ``sweep_fn(x_view, dms_slice, out, n_cols)`` are
-    injected by the CPU tests; the defaults are pdd_corner_turn and the HIP
-    DMSweep of this rank's slice (built once).
+    ``to_cm(src_tc, dst_cm_view)`` and ``sweep_fn(x, N, piece, x_off,
+    dms_slice, out, n_cols)`` (piece 0: x channel-major [C, N]) are injected
+    by the CPU tests; the defaults are pdd_corner_turn and the HIP DMSweep of
+    this rank's slice (built once).
     """
 
     def __init__(self, dms, freqs, dt, N, dtype=torch.uint8, n_batches=1, work=None,
-                 gather=False, dst=0, group=None, device=None, to_cm=None, sweep_fn=None):
+                 gather=False, dst=0, group=None, device=None, to_cm=None, sweep_fn=None,
+                 pieces=None):
         from . import delays as _delays
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -168,6 +173,10 @@ class DMShardedSweep(object):
         assert self.N % (self.nb * self.world) == 0, \
             "N must split into n_batches x world equal slices"
         self.T = self.N // self.nb
+        self.P = self.T // self.world
+        pow2 = self.P & (self.P - 1) == 0
+        self.pieces = pow2 if pieces is None else bool(pieces)
+        assert pow2 or not self.pieces, "the pieces layout needs a power-of-two slice length"
         tab = _delays.sweep_table(self.dms, self.freqs, dt)
         assert tab.size == 0 or tab.min() >= 0, "DM-sharded sweep expects delays >= 0"
         self.max_bin = int(tab.max()) if tab.size else 0
@@ -184,10 +193,19 @@ class DMShardedSweep(object):
         self.rows = self.hi - self.lo
         self.gather = bool(gather)
         self.dst = dst
-        # buffers (reused every call); one rank corner-turns its part directly
-        self.xt = (torch.empty((self.N, self.C), dtype=dtype, device=self.device)
-                   if self.world > 1 else None)                                    # time-major
-        self.x = torch.empty((self.C, self.N), dtype=dtype, device=self.device)   # channel-major
+        # buffers (reused every call)
+        if self.pieces:
+            # two corner-turn buffers: batch k+1's turn must not overwrite the
+            # one batch k's all-gather may still be reading
+            self.cm = [torch.empty((self.C, self.P), dtype=dtype, device=self.device)
+                       for _ in range(2)]
+            self.x = torch.empty((self.N // self.P, self.C, self.P), dtype=dtype,
+                                 device=self.device)
+            self.xt = None
+        else:
+            self.xt = (torch.empty((self.N, self.C), dtype=dtype, device=self.device)
+                       if self.world > 1 else None)
+            self.x = torch.empty((self.C, self.N), dtype=dtype, device=self.device)
         cols = [edges[k + 1] - edges[k] for k in range(self.nb)]
         if self.gather and self.rank == self.dst:
             # dst's full batch planes; its own rows are views of them
@@ -206,38 +224,59 @@ class DMShardedSweep(object):
             if self.rows:
                 self.sw = DMSweep(self.dms[self.lo:self.hi], self.freqs, dt, dtype=code)
 
-            def sweep_fn(xv, dms_slice, out, n_cols):
-                self.sw(xv, out=out, n_out=n_cols)
+            def sweep_fn(x, N, piece, x_off, dms_slice, out, n_cols):
+                if piece:
+                    self.sw.sweep_pieces(x, N, piece, x_off, n_cols, out)
+                else:
+                    self.sw(x[:, x_off:x_off + n_cols + self.max_bin], out=out, n_out=n_cols)
         self.sweep_fn = sweep_fn
 
     def __call__(self, part):
         """Run one pipelined sweep of the block whose per-rank slices are
-        ``part`` ([n_batches, T/W, C]).  Returns this rank's batch planes
+        ``part`` ([n_batches, P, C]).  Returns this rank's batch planes
         (with ``gather``: the full [D, cols_k] batch planes on ``dst``)."""
-        nb, W = self.nb, self.world
-        assert tuple(part.shape) == (nb, self.T // W, self.C) and part.dtype == self.dtype
-        T = self.T
+        nb, W, T, P = self.nb, self.world, self.T, self.P
+        assert tuple(part.shape) == (nb, P, self.C) and part.dtype == self.dtype
+        sends = []
 
-        def issue(k):
+        def exchange(k):
+            """Batch k into x: (corner turn +) all-gather; returns the pending
+            collective (None when done)."""
+            if self.pieces:
+                dst = self.x[k * W:(k + 1) * W]  # [W, C, P]
+                if W == 1:
+                    self.to_cm(part[k], dst[0])
+                    return None
+                cm = self.cm[k % 2]
+                self.to_cm(part[k], cm)
+                return _all_gather_into(dst.view(W * self.C, P), cm, group=self.group,
+                                        async_op=True)
             if W == 1:
+                self.to_cm(part[k], self.x[:, k * T:(k + 1) * T])
                 return None
             return _all_gather_into(self.xt[k * T:(k + 1) * T], part[k], group=self.group,
                                     async_op=True)
 
-        sends = []
-        pending = issue(0)
-        for k in range(nb):
-            if pending is not None:
-                pending.wait()
-            pending = issue(k + 1) if k + 1 < nb else None
-            rows = part[k] if W == 1 else self.xt[k * T:(k + 1) * T]
-            self.to_cm(rows, self.x[:, k * T:(k + 1) * T])
+        def sweep(k):
+            if not self.pieces and W > 1:
+                self.to_cm(self.xt[k * T:(k + 1) * T], self.x[:, k * T:(k + 1) * T])
             a, b = self.col_edges[k], self.col_edges[k + 1]
             if self.rows and b > a:
-                self.sweep_fn(self.x[:, a:b + self.max_bin], self.dms[self.lo:self.hi],
-                              self.planes[k], b - a)
+                self.sweep_fn(self.x, self.N, P if self.pieces else 0, a,
+                              self.dms[self.lo:self.hi], self.planes[k], b - a)
             if self.gather:
-                sends += self._gather_batch(k)
+                sends.extend(self._gather_batch(k))
+
+        pending = [None] * nb
+        for k in range(nb):
+            pending[k] = exchange(k)      # batch k's exchange overlaps batch k-1's sweep
+            if k > 0:
+                if pending[k - 1] is not None:
+                    pending[k - 1].wait()
+                sweep(k - 1)
+        if pending[nb - 1] is not None:
+            pending[nb - 1].wait()
+        sweep(nb - 1)
         for w in sends:
             w.wait()
         return self.full if (self.gather and self.rank == self.dst) else self.planes

@@ -127,6 +127,23 @@ class DMSweep(object):
              ptr(out), out.stride(0), n_out, stream_ptr(stream))
         return out
 
+    def sweep_pieces(self, xp, N, piece, x_off, n_out, out, stream=None):
+        """Plane columns [x_off, x_off + n_out) of the sweep of a block held
+        in the "pieces" layout an all-gather of channel-major time slices
+        produces: ``xp`` memory = [ceil(N/piece)][C][piece] (piece a power of
+        two), sample s of channel c at xp[(s//piece)*C*piece + c*piece +
+        s%piece] (pdd_sweep_execute_ex).  Pads are value 0 (trim=True grids
+        with delays >= 0 never read them)."""
+        code = _lib.U8 if xp.dtype == torch.uint8 else _lib.F32
+        if code == _lib.U8 and self.dtype != "u8":
+            raise TypeError("8-bit pieces need a dtype='u8' DMSweep")
+        assert out.shape[0] == self.D and out.shape[1] >= n_out and out.stride(1) == 1
+        assert xp.is_contiguous() and xp.numel() >= -(-N // piece) * self.C * piece
+        pv = torch.zeros(self.C, dtype=torch.float32, device=xp.device)
+        call("pdd_sweep_execute_ex", self._plan(code), ptr(xp), N, 0, piece, x_off, _lib.PAD_VALUE,
+             ptr(pv), ptr(out), out.stride(0), n_out, stream_ptr(stream))
+        return out
+
     def set_timing(self, on=True, code=None):
         """Bracket the sweep kernel of every execute with HIP events (on the
         execute stream); read the last duration with kernel_ms()."""

@@ -434,3 +434,29 @@ def test_grouped_u8_sweep(gpu, pad):
                                n_out=n_out)
         np.testing.assert_array_equal(got[g * 10:(g + 1) * 10], want)
     gs.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["u8", "f32"])
+def test_sweep_pieces_layout_and_offset(gpu, dtype):
+    """pdd_sweep_execute_ex: a block in the all-gathered "pieces" layout
+    [N/P][C][P] and a column offset give exactly those columns of the
+    channel-major one-shot plane (the DM-sharded path's input)."""
+    import torch
+    from pypulsar_amd.sweep import DMSweep
+    C, N, P = 48, 16384, 2048
+    freqs = band(C)
+    dms = np.linspace(0.0, 60.0, 37)
+    x = u8_data(C, N, 23)
+    xd = torch.from_numpy(x).cuda()
+    if dtype == "f32":
+        xd = xd.float()
+    sw = DMSweep(dms, freqs, DT, dtype=dtype)
+    full = sw(xd)
+    n_out = full.shape[1]
+    xp = xd.reshape(C, N // P, P).permute(1, 0, 2).contiguous()  # [N/P][C][P]
+    for x_off, cols in ((0, n_out), (3000, 5000), (n_out - 777, 777)):
+        out = torch.full((len(dms), cols), -1.0, device="cuda")
+        sw.sweep_pieces(xp, N, P, x_off, cols, out)
+        assert torch.equal(out, full[:, x_off:x_off + cols]), (x_off, cols)
+    sw.close()

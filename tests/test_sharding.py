@@ -49,7 +49,7 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        C, N, NB = 16, 1000, 2400
+        C, N, NB, NBP = 16, 1000, 2400, 4096
         freqs = _band(C)
         dms = np.linspace(0.0, 40.0, 11)
         from oracle import spectra_oracle as orc
@@ -82,32 +82,49 @@ def _worker(rank, world, port, q):
         # pipelined DM sharding (DMShardedSweep): per-rank H2D slices of every
         # time batch, all-gathered batch by batch; planes resident (ag) or
         # gathered to rank 0 batch by batch (agg); DM slices work-weighted
-        xt = torch.from_numpy(_data(C, NB).T.copy())  # [NB, C] time-major
         work = np.r_[np.ones(5), np.full(len(dms) - 5, 0.5)]
 
         def to_cm(src_tc, dst_cm):
             dst_cm.copy_(src_tc.t())
 
-        def sweep_fn(xv, sub, out, n_cols):
+        def sweep_fn(x, N, piece, x_off, sub, out, n_cols):
+            if piece:  # [N/P][C][P] pieces -> channel-major
+                x = x.reshape(N // piece, C, piece).permute(1, 0, 2).reshape(C, N)
             tab = orc.sweep_table(sub, freqs, DT)
+            xv = x[:, x_off:x_off + n_cols + int(tab.max())]
             out.copy_(torch.from_numpy(orc.sweep_plane(xv.numpy().astype(np.float64), tab,
                                                        n_out=n_cols).astype(np.float32)))
         res = {}
-        for gather in (False, True):
-            ds = sharding.DMShardedSweep(dms, freqs, DT, NB, dtype=torch.float32, n_batches=2,
+        # NB = 2400 splits into 2 batches x world slices of 600 or 400 spectra
+        # (time-major path); NBP = 4096 into power-of-two slices (pieces path)
+        cases = [(False, NB, False), (True, NB, False)]
+        if world in (1, 2, 4, 8):  # power-of-two slices of NBP: the pieces path
+            cases += [(False, NBP, True), (True, NBP, True)]
+        for gather, nbk, pieces in cases:
+            xs = torch.from_numpy(_data(C, nbk).T.copy())
+            ds = sharding.DMShardedSweep(dms, freqs, DT, nbk, dtype=torch.float32, n_batches=2,
                                          work=work, gather=gather, to_cm=to_cm,
                                          sweep_fn=sweep_fn)
-            part = sharding.split_block(xt, 2, world, rank)
+            assert ds.pieces == pieces
+            part = sharding.split_block(xs, 2, world, rank)
             for _ in range(2):  # a second step reuses every buffer
                 ds(part)
-            res[gather] = (ds.lo, ds.hi, ds.plane().numpy(), ds.slices)
+            res[(gather, pieces)] = (ds.lo, ds.hi, ds.plane().numpy(), ds.slices)
         ag = [None] * world
-        dist.all_gather_object(ag, res[False][:3])
+        dist.all_gather_object(ag, res[(False, False)][:3])
+        agp = [None] * world
+        dist.all_gather_object(agp, res.get((False, True), (0, 0, None))[:3])
         # plane gather into a preallocated plane (no concatenation)
-        g = sharding.gather_planes(torch.from_numpy(res[False][2]), res[False][3])
+        g = sharding.gather_planes(torch.from_numpy(res[(False, False)][2]), res[(False, False)][3])
         if rank == 0:
             q.put(("ag", np.concatenate([p for _, _, p in sorted(ag, key=lambda a: a[0])])))
-            q.put(("agg", res[True][2]))
+            q.put(("agg", res[(True, False)][2]))
+            if (False, True) in res:
+                q.put(("agp", np.concatenate([p for _, _, p in sorted(agp, key=lambda a: a[0])])))
+                q.put(("aggp", res[(True, True)][2]))
+            else:
+                q.put(("agp", None))
+                q.put(("aggp", None))
             q.put(("gp", g.numpy()))
             q.put(("dm", plane.numpy()))
             q.put(("tb", np.concatenate(parts, axis=1)))
@@ -125,7 +142,7 @@ def test_sharded_sweeps_equal_one_shot(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=240) for _ in range(6))
+    got = dict(q.get(timeout=240) for _ in range(8))
     for p in procs:
         p.join(timeout=240)
         assert p.exitcode == 0
@@ -141,6 +158,10 @@ def test_sharded_sweeps_equal_one_shot(world):
     np.testing.assert_array_equal(got["ag"].astype(np.float64), want_b)
     np.testing.assert_array_equal(got["agg"].astype(np.float64), want_b)
     np.testing.assert_array_equal(got["gp"].astype(np.float64), want_b)
+    if world in (1, 2, 4, 8):
+        want_p = orc.sweep_plane(_data(C, 4096).astype(np.float64), tab)
+        np.testing.assert_array_equal(got["agp"].astype(np.float64), want_p)
+        np.testing.assert_array_equal(got["aggp"].astype(np.float64), want_p)
     # sharded search == search of the one-shot plane
     from oracle import search_oracle as so
     xs = _data(C, N)
