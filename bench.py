@@ -238,6 +238,8 @@ def main():
                     help="dmshard: time batches per step (default 1 on one GPU, 4 otherwise)")
     ap.add_argument("--gather", action="store_true",
                     help="dmshard: also gather every batch's plane rows to rank 0 (p2p)")
+    ap.add_argument("--zdm", default="auto", choices=["auto", "int", "wrap", "float", "none"],
+                    help="stream: zero-DM mode (auto = exact integer 16-bit path for 8-bit data)")
     ap.add_argument("--cpu-trials", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true",
@@ -640,8 +642,10 @@ def search_bench(args, cfg, rank, world, dev):
 
 def stream_bench(args, cfg, rank, world, dev):
     """BASELINE configs[4]: continuous 8-bit blocks [block, C] from PINNED host
-    memory -> async H2D (copy stream) -> fused zero-DM (float) + downsample 2
-    -> 2048-DM sweep (pypulsar_amd.stream).  One step = one block through the
+    memory -> async H2D (copy stream) -> fused zero-DM + downsample 2 ->
+    2048-DM sweep (pypulsar_amd.stream; default zero-DM mode 'int': the
+    reference's rounded channel mean subtracted exactly, swept on the exact
+    16-bit path; --zdm float for the float32 path).  One step = one block through the
     whole pipeline, H2D included.  Each rank streams its own data (weak)."""
     from pypulsar_amd.stream import StreamingSweep
     C, D, ds = cfg["C"], cfg["D"], cfg["ds"]
@@ -652,10 +656,10 @@ def stream_bench(args, cfg, rank, world, dev):
     if args.search:
         from pypulsar_amd.search import StreamingSearch
         ss = StreamingSearch(dms, freqs, dt, block=block, downsamp=ds, threshold=8.0,
-                             detrendlen=1024)
+                             detrendlen=1024, zero_dm=args.zdm)
         st = ss.sweep
     else:
-        st = StreamingSweep(dms, freqs, dt, block=block, downsamp=ds)
+        st = StreamingSweep(dms, freqs, dt, block=block, downsamp=ds, zero_dm=args.zdm)
     # two distinct pinned chunks, reused cyclically (content is irrelevant to speed)
     chunks = []
     for i in range(2):
@@ -705,8 +709,9 @@ def stream_bench(args, cfg, rank, world, dev):
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic uint8 clip(round(N(128,16))) blocks in pinned host memory",
         "config": {"workload": "streaming: %d-ch u8 blocks of %d spectra (pinned H2D, async) + "
-                               "zero-DM (float) + downsample %d + %d-DM sweep (0-%g pc/cc)%s"
-                               % (C, block, ds, D, cfg["dm_hi"],
+                               "zero-DM (%s) + downsample %d + %d-DM sweep (0-%g pc/cc, %s)%s"
+                               % (C, block, st.mode, ds, D, cfg["dm_hi"],
+                                  "exact u16" if st.exact else "float32",
                                   " + boxcar search (13 widths, S/N 8)" if args.search else ""),
                    "candidates": ncand if args.search else None,
                    "config_name": "stream", "channels": C, "block": block, "overlap": st.ov,

@@ -111,6 +111,23 @@ int pdd_zero_dm(const void* in, int dtype, int64_t nspec, int64_t nchan, int64_t
 int pdd_zdm_downsample(const void* in, int dtype, int64_t nspec, int64_t nchan, int64_t ld,
                        int64_t factor, int zero_dm, float* out, int64_t ld_out, void* stream);
 
+/* The 8-bit prologue of the exact 16-bit sweep (streaming configs[4]): the
+ * same zero-DM + downsample + corner turn in integer arithmetic,
+ *   out[c][j] = offset + sum_{k<factor} z(x[j*factor+k][c]),  uint16, channel-major,
+ * with m = the spectrum's channel mean rounded half-to-even (np.round, as
+ * bin/zero_dm_filter.py:30-39) and z by mode:
+ *   PDD_ZDM_NONE  z = x                  (no filter; plain downsample)
+ *   PDD_ZDM_INT   z = x - m, signed      (integer zero-DM without the uint8 wrap)
+ *   PDD_ZDM_WRAP  z = (x - m) mod 256    (the reference's uint8 result exactly)
+ * 8-bit input with 16-byte-aligned rows (nchan % 16 == 0); offset must keep
+ * every value in [0, 65535] (PDD_ZDM_INT: offset >= 255 factor).  For the
+ * 16-bit sweep (values <= 1023): factor <= 2 for PDD_ZDM_INT (offset 255
+ * factor), <= 4 otherwise (offset 0). */
+enum { PDD_ZDM_NONE = 0, PDD_ZDM_INT = 1, PDD_ZDM_WRAP = 2 };
+int pdd_zdm_int_downsample(const void* in, int dtype, int64_t nspec, int64_t nchan, int64_t ld,
+                           int64_t factor, int mode, int offset, uint16_t* out, int64_t ld_out,
+                           void* stream);
+
 /* ---- waterfaller post-chain (Spectra.scaled / scaled2 / masked / smooth) ---- */
 /* Whole-array statistics of x[C][N] into out4 (device float[4]):
  * {mean, population std, min, max}, float64 accumulation.
@@ -142,12 +159,15 @@ int pdd_smooth(const float* x, int64_t C, int64_t N, int64_t ld, int64_t width, 
 typedef struct pdd_sweep_plan pdd_sweep_plan;
 
 /* host_table: [D][C] int32, row d = the bins Spectra.dedisperse(dms[d])
- * would pass to shift_channels.  dtype: PDD_F32 or PDD_U8 input. */
+ * would pass to shift_channels.  dtype: PDD_F32, PDD_U8 or PDD_U16 (samples
+ * <= 1023) input. */
 int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int dtype,
                           pdd_sweep_plan** plan);
 /* x: [C][N] (ld) of the plan's dtype; out: [D][ld_out] float32.
  * For PDD_U8 with PDD_PAD_VALUE every padvals[c] must be an integer in
- * [0, 255] (checked on the host side by the caller). */
+ * [0, 255] (checked on the host side by the caller).  PDD_U16 input: unsigned
+ * 16-bit samples <= 1023 (e.g. the offset output of pdd_zdm_int_downsample),
+ * swept exactly with the packed-u16 kernels. */
 int pdd_sweep_execute(const pdd_sweep_plan* plan, const void* x, int64_t N, int64_t ld,
                       int pad_mode, const float* padvals, float* out, int64_t ld_out,
                       int64_t n_out, void* stream);
@@ -158,12 +178,14 @@ int pdd_sweep_execute(const pdd_sweep_plan* plan, const void* x, int64_t N, int6
  *     (sample s of channel c at x[(s/P)*C*P + c*P + s%P]);
  *   x_off: plane column t sums input samples t + x_off + table[d][c] (a column
  *     range [x_off, x_off + n_out) of the full sweep); pads apply outside
- *     [0, N) of x.
+ *     [0, N) of x;
+ *   out_bias: added to every plane value (e.g. -offset * C for offset input). 
  * Offsets and pieces need the interleaved tilings (every grid whose shift
  * span per trial block fits the LDS); sparser grids return an error. */
 int pdd_sweep_execute_ex(const pdd_sweep_plan* plan, const void* x, int64_t N, int64_t ld,
                          int64_t piece, int64_t x_off, int pad_mode, const float* padvals,
-                         float* out, int64_t ld_out, int64_t n_out, void* stream);
+                         float* out, int64_t ld_out, int64_t n_out, float out_bias,
+                         void* stream);
 /* Grouped sweep: n_grp independent channel groups of C channels each
  * (channels g*C .. g*C+C-1 of the input), every group with its own [D][C]
  * table: host_table is [n_grp][D][C].  One launch replaces n_grp sweeps --

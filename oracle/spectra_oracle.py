@@ -339,3 +339,25 @@ def zdm_downsample(block_tc, factor, zero_dm=True):
         x = x - x.mean(axis=1, keepdims=True)
     n = (x.shape[0] // factor) * factor
     return x[:n].reshape(n // factor, factor, x.shape[1]).sum(axis=1).T
+
+
+def zdm_int_downsample(block_tc, factor, mode="int"):
+    """Integer prologue of the stream's exact 16-bit path: [nspec, nchan]
+    uint8 -> [nchan, nspec // factor] int64 co-added values, zero-DM by mode:
+      'wrap': zero_dm_block (bin/zero_dm_filter.py:30-39 on uint8 data,
+              the reference's result exactly: wraps modulo 256);
+      'int':  x - np.round(mean) as a signed integer (the reference's rounded
+              mean, :35-38, without the uint8 cast of the difference);
+      'none': x.
+    Downsample = co-add of ``factor`` spectra (formats/spectra.py:329-351)."""
+    x = np.asarray(block_tc)
+    assert x.dtype == np.uint8
+    if mode == "wrap":
+        z = zero_dm_block(x).astype(np.int64)
+    elif mode == "int":
+        avg = np.array([np.round(row.mean()) for row in x])  # per spectrum, as :35-38
+        z = x.astype(np.int64) - avg.astype(np.int64)[:, None]
+    else:
+        z = x.astype(np.int64)
+    n = (z.shape[0] // factor) * factor
+    return z[:n].reshape(n // factor, factor, z.shape[1]).sum(axis=1).T

@@ -23,6 +23,7 @@ F32, U8, U16 = 0, 1, 2
 PAD_VALUE, PAD_ROTATE = 0, 1
 STAT_MEAN, STAT_MEDIAN, STAT_STD, STAT_MIN, STAT_MAX = 0, 1, 2, 3, 4
 LAYOUT_TIME_MAJOR, LAYOUT_CHAN_MAJOR = 0, 1
+ZDM_NONE, ZDM_INT, ZDM_WRAP = 0, 1, 2
 
 # every symbol include/pdd.h declares (checked by tests/test_abi.py)
 EXPORTS = (
@@ -33,7 +34,7 @@ EXPORTS = (
     "pdd_smooth", "pdd_zdm_downsample", "pdd_sweep_set_timing", "pdd_sweep_kernel_ms",
     "pdd_sweep_plan_create_grouped", "pdd_sweep_execute_grouped", "pdd_sp_chunk_stats",
     "pdd_sp_search", "pdd_psrfits_subints", "pdd_downsample_u8", "pdd_sweep_timing_read",
-    "pdd_sweep_execute_ex",
+    "pdd_sweep_execute_ex", "pdd_zdm_int_downsample",
 )
 
 
@@ -63,8 +64,8 @@ _SIGS = {
     "pdd_zero_dm": ([_vp, _int, _i64, _i64, _i64, _int, _vp, _i64, _vp], _int),
     "pdd_sweep_plan_create": ([_vp, _i64, _i64, _int, ctypes.POINTER(_vp)], _int),
     "pdd_sweep_execute": ([_vp, _vp, _i64, _i64, _int, _vp, _vp, _i64, _i64, _vp], _int),
-    "pdd_sweep_execute_ex": ([_vp, _vp, _i64, _i64, _i64, _i64, _int, _vp, _vp, _i64, _i64, _vp],
-                             _int),
+    "pdd_sweep_execute_ex": ([_vp, _vp, _i64, _i64, _i64, _i64, _int, _vp, _vp, _i64, _i64,
+                              ctypes.c_float, _vp], _int),
     "pdd_sweep_plan_info": ([_vp, _vp], _int),
     "pdd_sweep_plan_destroy": ([_vp], _int),
     "pdd_global_stats": ([_vp, _i64, _i64, _i64, _vp, _vp], _int),
@@ -72,6 +73,8 @@ _SIGS = {
     "pdd_masked_fill": ([_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _i64, _vp], _int),
     "pdd_smooth": ([_vp, _i64, _i64, _i64, _i64, _int, _vp, _vp, _i64, _vp], _int),
     "pdd_zdm_downsample": ([_vp, _int, _i64, _i64, _i64, _i64, _int, _vp, _i64, _vp], _int),
+    "pdd_zdm_int_downsample": ([_vp, _int, _i64, _i64, _i64, _i64, _int, _int, _vp, _i64, _vp],
+                               _int),
     "pdd_sweep_set_timing": ([_vp, _int], _int),
     "pdd_sweep_plan_create_grouped": ([_vp, _i64, _i64, _i64, _int, ctypes.POINTER(_vp)], _int),
     "pdd_sweep_execute_grouped": ([_vp, _vp, _i64, _i64, _int, _vp, _vp, _i64, _i64, _i64, _i64,

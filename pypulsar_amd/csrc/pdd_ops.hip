@@ -867,6 +867,61 @@ __global__ __launch_bounds__(256) void k_zdm_ds_vec(const T* __restrict__ in, in
   }
 }
 
+// 8-bit prologue of the exact 16-bit sweep: zero-DM (bin/zero_dm_filter.py:
+// 30-39, the spectrum's channel mean rounded half-to-even as np.round) +
+// downsample (formats/spectra.py:329-351, co-added) + corner turn, 16-B
+// aligned rows:
+//   out[c][j] = offset + sum_{k < f} z(x[j f + k][c], m[j f + k])
+// as uint16, z = x (MODE 0: no filter), x - m as a signed value (MODE 1:
+// integer zero-DM without the uint8 wrap) or (x - m) mod 256 (MODE 2: the
+// reference's uint8 arithmetic).  Integer math throughout (exact); the tile
+// order is that of k_zdm_ds_vec.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_zdm_int_ds_vec(const uint8_t* __restrict__ in,
+                                                        int64_t nchan, int64_t ld,
+                                                        const double* __restrict__ mean, int f,
+                                                        uint16_t* __restrict__ out, int64_t ld_out,
+                                                        int64_t nout, int64_t tiles_c, int offset) {
+  constexpr int VEC = 16;
+  constexpr int TC = 8 * VEC;
+  __shared__ int tile[TC][65];
+  const int64_t tj = blockIdx.x / tiles_c, tc = blockIdx.x % tiles_c;
+  const int64_t j0 = tj * 64, c0 = tc * TC;
+  const int seg = threadIdx.x & 7, r0 = threadIdx.x >> 3;
+  const int64_t c = c0 + seg * VEC;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int jl = r0 + 32 * pass;
+    const int64_t j = j0 + jl;
+    int acc[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc[e] = offset;
+    if (j < nout && c < nchan) {
+      for (int k = 0; k < f; ++k) {
+        const int64_t t = j * f + k;
+        union { uint4 q; uint8_t e[VEC]; } u;
+        u.q = *reinterpret_cast<const uint4*>(in + t * ld + c);
+        const int m = MODE ? (int)rint(mean[t]) : 0;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          const int z = (int)u.e[e] - m;
+          acc[e] += MODE == 2 ? (z & 255) : z;
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) tile[seg * VEC + e][jl] = acc[e];
+  }
+  __syncthreads();
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t j = j0 + tx;
+#pragma unroll 4
+  for (int i = ty; i < TC; i += 4) {
+    const int64_t cc = c0 + i;
+    if (j < nout && cc < nchan) out[cc * ld_out + j] = (uint16_t)tile[i][tx];
+  }
+}
+
 static int grid_1d(int64_t n, int per_block = 256) {
   int64_t g = cdiv(n, per_block);
   if (g > 2048 * 8) g = 2048 * 8;
@@ -1225,6 +1280,49 @@ int pdd_zdm_downsample(const void* in, int dtype, int64_t nspec, int64_t nchan, 
   const hipError_t e = hipGetLastError();
   if (mean) (void)hipFreeAsync(mean, s);
   PDD_REQUIRE(e == hipSuccess, "pdd_zdm_downsample: launch failed: %s", hipGetErrorString(e));
+  return 0;
+}
+
+int pdd_zdm_int_downsample(const void* in, int dtype, int64_t nspec, int64_t nchan, int64_t ld,
+                           int64_t factor, int mode, int offset, uint16_t* out, int64_t ld_out,
+                           void* stream) {
+  PDD_REQUIRE(in && out, "pdd_zdm_int_downsample: null pointer");
+  PDD_REQUIRE(dtype == PDD_U8, "pdd_zdm_int_downsample: 8-bit input only");
+  PDD_REQUIRE(mode >= PDD_ZDM_NONE && mode <= PDD_ZDM_WRAP, "pdd_zdm_int_downsample: bad mode %d",
+              mode);
+  PDD_REQUIRE(nspec >= 0 && nchan > 0 && ld >= nchan, "pdd_zdm_int_downsample: bad shape");
+  PDD_REQUIRE(factor >= 1 && factor <= 64 && 64 % factor == 0,
+              "pdd_zdm_int_downsample: factor must divide 64");
+  const int lo = mode == PDD_ZDM_INT ? -255 * (int)factor : 0, hi = 255 * (int)factor;
+  PDD_REQUIRE(offset + lo >= 0 && offset + hi <= 65535,
+              "pdd_zdm_int_downsample: offset %d cannot hold [%d, %d] in uint16", offset, lo, hi);
+  PDD_REQUIRE(ld_out >= nspec / factor, "pdd_zdm_int_downsample: ld_out too small");
+  PDD_REQUIRE((uintptr_t)in % 16 == 0 && ld % 16 == 0 && nchan % 16 == 0,
+              "pdd_zdm_int_downsample: rows must be 16-byte aligned (nchan %% 16 == 0)");
+  if (nspec < factor) return 0;
+  hipStream_t s = as_stream(stream);
+  double* mean = nullptr;
+  if (mode != PDD_ZDM_NONE) {
+    PDD_HIP(hipMallocAsync((void**)&mean, (size_t)nspec * sizeof(double), s));
+    k_spectrum_mean_vec<uint8_t><<<(unsigned)cdiv(nspec, 4), 256, 0, s>>>(
+        (const uint8_t*)in, nspec, nchan, ld, mean);
+  }
+  const int64_t nout = nspec / factor;
+  const int64_t tcv = cdiv(nchan, 8 * 16);
+  const dim3 grid((unsigned)(cdiv(nout, 64) * tcv));
+  const uint8_t* x = (const uint8_t*)in;
+  if (mode == PDD_ZDM_NONE)
+    k_zdm_int_ds_vec<0><<<grid, 256, 0, s>>>(x, nchan, ld, mean, (int)factor, out, ld_out, nout,
+                                             tcv, offset);
+  else if (mode == PDD_ZDM_INT)
+    k_zdm_int_ds_vec<1><<<grid, 256, 0, s>>>(x, nchan, ld, mean, (int)factor, out, ld_out, nout,
+                                             tcv, offset);
+  else
+    k_zdm_int_ds_vec<2><<<grid, 256, 0, s>>>(x, nchan, ld, mean, (int)factor, out, ld_out, nout,
+                                             tcv, offset);
+  const hipError_t e = hipGetLastError();
+  if (mean) (void)hipFreeAsync(mean, s);
+  PDD_REQUIRE(e == hipSuccess, "pdd_zdm_int_downsample: launch failed: %s", hipGetErrorString(e));
   return 0;
 }
 

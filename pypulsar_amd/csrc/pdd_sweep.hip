@@ -501,10 +501,12 @@ __global__ __launch_bounds__(256) void k_interleave(const InT* __restrict__ x, I
   }
 }
 
-// u16 eighths for 8-bit data: R[c][j] = 8 samples X(c, b + j + k*Qs), k < 8,
-// as packed u16 pairs (word h = sample 2h | sample 2h+1 << 16); pads (integer
-// values 0..255, checked by the caller) and rotation baked in as for float32.
-__global__ __launch_bounds__(256) void k_interleave_u16(const uint8_t* __restrict__ x, InLayout lay,
+// u16 eighths for 8-bit data (and for 16-bit data <= 1023): R[c][j] = 8
+// samples X(c, b + j + k*Qs), k < 8, as packed u16 pairs (word h = sample 2h |
+// sample 2h+1 << 16); pads (integer values, checked by the caller) and
+// rotation baked in as for float32.
+template <typename InT>
+__global__ __launch_bounds__(256) void k_interleave_u16(const InT* __restrict__ x, InLayout lay,
                                                         int64_t N, int64_t base, int64_t Qs,
                                                         int64_t nR, int pad_mode,
                                                         const float* __restrict__ padvals,
@@ -632,7 +634,8 @@ template <int G, int DPW, int NCW, int NLW, int CC, int NBUF, bool U16 = false>
 __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const float4* __restrict__ R0, int64_t nR, int C, int lo, const int* __restrict__ mt,
     float* __restrict__ out, int64_t ld_out, int D, int64_t Qs, int64_t t_base, int64_t n_out,
-    int stride, int n_tblk, int n_dblk, int dbg, int64_t row_g, int64_t row_d) {
+    int stride, int n_tblk, int n_dblk, int dbg, int64_t row_g, int64_t row_d, int flush_n,
+    float out_bias) {
   // Grouped sweeps: C is the channel count of ONE group; blockIdx.x / (tiles
   // per group) is the group, whose channels are R rows [grp*C, grp*C + C),
   // whose tables are mt[grp][...], and whose trial d lands in plane row
@@ -750,7 +753,8 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   // u16 elements (8-bit data): 8 eighth samples per read as packed u16 pairs,
   // accumulated with plain 32-bit adds (two u16 lanes per add, no carry while
   // <= 257 channels of values <= 255 are summed) and flushed to float every
-  // 256 channels -- exact.
+  // flush_n channels (256 for 8-bit data, 64 for 16-bit data <= 1023) --
+  // exact.
   // accumulators as float pairs: the adds issue as v_pk_add_f32 (two samples
   // per VALU instruction: half the issue slots of scalar v_add_f32)
   typedef float f32x2_t __attribute__((ext_vector_type(2)));
@@ -836,7 +840,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
               }
             __builtin_amdgcn_sched_barrier(0);
           }
-          if (++since_flush == 256) {
+          if (++since_flush == flush_n) {
             since_flush = 0;
             flush16();
           }
@@ -888,7 +892,8 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const int64_t t = t0 + g * 64 + lane;
-        if (t < Qs && t_base + t + k2 * Qs < n_out) orow[t + k2 * Qs] = acc[j][g][k2 >> 1][k2 & 1];
+        if (t < Qs && t_base + t + k2 * Qs < n_out)
+          orow[t + k2 * Qs] = acc[j][g][k2 >> 1][k2 & 1] + out_bias;
       }
   }
 }
@@ -1288,7 +1293,8 @@ static int64_t lds_budget(const Variant& v) {
 static constexpr int kLdsMax = 160 * 1024;
 
 typedef void (*sweep_il_fn)(const float4*, int64_t, int, int, const int*, float*, int64_t, int,
-                            int64_t, int64_t, int64_t, int, int, int, int, int64_t, int64_t);
+                            int64_t, int64_t, int64_t, int, int, int, int, int64_t, int64_t, int,
+                            float);
 static sweep_il_fn il_kernel_for(const Variant& v) {
 #define IL(NCW_, NLW_, CC_, NB_)                                                              \
   if (v.S == 4 && v.NW == NCW_ && v.NLW == NLW_ && v.CC == CC_ && v.NBUF == NB_ && v.G == 4 && \
@@ -1564,11 +1570,14 @@ static int execute_mx(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
 // after the segment loop); each segment is one k_interleave + one k_sweep_il.
 static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayout lay,
                       int64_t x_off, int pad_mode, const float* padvals, float* out,
-                      int64_t ld_out, int64_t n_out, int64_t row_g, int64_t row_d, void* stream) {
+                      int64_t ld_out, int64_t n_out, int64_t row_g, int64_t row_d, float out_bias,
+                      void* stream) {
   const int Tq = 64 * p->v.G;
   const int SP = p->v.S;  // samples per element: 4 (float32 quarters) or 8 (u16 eighths)
   const bool u16 = (SP == 8);
-  PDD_REQUIRE(!u16 || p->dtype == PDD_U8, "pdd_sweep_execute: u16 path needs 8-bit input");
+  PDD_REQUIRE(!u16 || p->dtype != PDD_F32, "pdd_sweep_execute: u16 path needs integer input");
+  // packed u16 lanes: 257 channels of 8-bit values, 64 of 16-bit values <= 1023
+  const int flush_n = p->dtype == PDD_U8 ? 256 : 64;
   const int64_t C = p->C * p->n_grp;  // all channels (groups are contiguous channel ranges)
   const int64_t lo = std::min(0, p->min_bin), hi = std::max(0, p->max_bin);
   int64_t budget = (int64_t)8 << 30;  // bytes of R per segment
@@ -1593,9 +1602,15 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
     const int64_t Qs = cdiv(cdiv(cnt, SP), Tq) * Tq;
     const int64_t nR = Qs + (hi - lo) + 64;
     dim3 g1((unsigned)cdiv(nR, 256 * kIlPer), (unsigned)C);
-    if (u16)
-      hipLaunchKernelGGL(k_interleave_u16, g1, dim3(256), 0, st, (const uint8_t*)x, lay, N,
+    if (u16 && p->dtype == PDD_U8)
+      hipLaunchKernelGGL(k_interleave_u16<uint8_t>, g1, dim3(256), 0, st, (const uint8_t*)x, lay, N,
                          t_base + lo + x_off, Qs, nR, pad_mode, padvals, (uint4*)R);
+    else if (u16)
+      hipLaunchKernelGGL(k_interleave_u16<uint16_t>, g1, dim3(256), 0, st, (const uint16_t*)x, lay,
+                         N, t_base + lo + x_off, Qs, nR, pad_mode, padvals, (uint4*)R);
+    else if (p->dtype == PDD_U16)
+      hipLaunchKernelGGL(k_interleave<uint16_t>, g1, dim3(256), 0, st, (const uint16_t*)x, lay, N,
+                         t_base + lo + x_off, Qs, nR, pad_mode, padvals, R);
     else if (p->dtype == PDD_U8)
       hipLaunchKernelGGL(k_interleave<uint8_t>, g1, dim3(256), 0, st, (const uint8_t*)x, lay, N,
                          t_base + lo + x_off, Qs, nR, pad_mode, padvals, R);
@@ -1613,7 +1628,7 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
     hipLaunchKernelGGL(il_kernel_for(p->v), dim3((unsigned)blocks), dim3(p->v.threads()),
                        p->lds_bytes, st, R, nR, (int)p->C, (int)lo, p->d_tab, out, ld_out,
                        (int)p->D, Qs, t_base, t_base + cnt, p->stride, (int)n_tblk,
-                       (int)p->n_dblk, dbg, row_g, row_d);
+                       (int)p->n_dblk, dbg, row_g, row_d, flush_n, out_bias);
     if (hipGetLastError() != hipSuccess) rc = -3;
     if (bracket) {
       (void)hipEventRecord(p->ev[2 * p->timed + 1], st);
@@ -1639,10 +1654,13 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
   PDD_REQUIRE(n_grp >= 1 && n_grp * C < (1 << 20), "pdd_sweep_plan_create: bad group count");
   PDD_REQUIRE(D > 0 && C > 0 && D < (1 << 24) && C < (1 << 20),
               "pdd_sweep_plan_create: bad extents D=%lld C=%lld", (long long)D, (long long)C);
-  PDD_REQUIRE(dtype == PDD_F32 || dtype == PDD_U8, "pdd_sweep_plan_create: dtype must be F32 or U8");
-  const Variant* cands = dtype == PDD_U8 ? kU8Variants : kF32Variants;
-  const int ncand = dtype == PDD_U8 ? (int)(sizeof(kU8Variants) / sizeof(Variant))
-                                    : (int)(sizeof(kF32Variants) / sizeof(Variant));
+  PDD_REQUIRE(dtype == PDD_F32 || dtype == PDD_U8 || dtype == PDD_U16,
+              "pdd_sweep_plan_create: dtype must be F32, U8 or U16");
+  // 16-bit input (<= 1023) shares the 8-bit tilings minus the generic kernel
+  const bool int_in = dtype != PDD_F32;
+  const Variant* cands = int_in ? kU8Variants : kF32Variants;
+  const int ncand = int_in ? (int)(sizeof(kU8Variants) / sizeof(Variant))
+                           : (int)(sizeof(kF32Variants) / sizeof(Variant));
 
 #ifdef PDD_SWEEP_DEV
   if (dtype == PDD_U8 && n_grp == 1 && getenv("PDD_SWEEP_MX") && atoi(getenv("PDD_SWEEP_MX"))) {
@@ -1657,6 +1675,10 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
     const Variant v = cands[vi];
     const bool il = v.kind == 0;
     if (n_grp > 1 && !il) continue;  // only the interleaved kernel sweeps groups
+    if (dtype == PDD_U16 && !il) {     // the generic kernel reads 8-bit or float32 rows
+      set_error("pdd_sweep_plan_create: DM grid too sparse for a 16-bit-input tile");
+      return -1;
+    }
     const int64_t DB = v.DB();
     const int64_t n_dblk = cdiv(D, DB);
     const int64_t Dpad = n_dblk * DB;
@@ -1780,12 +1802,13 @@ int pdd_sweep_plan_info(const pdd_sweep_plan* p, int64_t* info) {
 int pdd_sweep_execute(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t ld, int pad_mode,
                       const float* padvals, float* out, int64_t ld_out, int64_t n_out,
                       void* stream) {
-  return pdd_sweep_execute_ex(p, x, N, ld, 0, 0, pad_mode, padvals, out, ld_out, n_out, stream);
+  return pdd_sweep_execute_ex(p, x, N, ld, 0, 0, pad_mode, padvals, out, ld_out, n_out, 0.f,
+                              stream);
 }
 
 int pdd_sweep_execute_ex(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t ld,
                          int64_t piece, int64_t x_off, int pad_mode, const float* padvals,
-                         float* out, int64_t ld_out, int64_t n_out, void* stream) {
+                         float* out, int64_t ld_out, int64_t n_out, float out_bias, void* stream) {
   PDD_REQUIRE(p && x && out, "pdd_sweep_execute: null pointer");
   PDD_REQUIRE(N > 0 && n_out >= 0 && ld_out >= n_out && x_off >= 0, "pdd_sweep_execute: bad shape");
   PDD_REQUIRE(piece > 0 || ld >= N, "pdd_sweep_execute: row stride %lld < N", (long long)ld);
@@ -1805,10 +1828,11 @@ int pdd_sweep_execute_ex(const pdd_sweep_plan* p, const void* x, int64_t N, int6
   }
 #endif
   if (p->v.kind == 0)
-    return execute_il(p, x, N, lay, x_off, pad_mode, padvals, out, ld_out, n_out, 0, 1, stream);
-  PDD_REQUIRE(piece == 0 && x_off == 0,
+    return execute_il(p, x, N, lay, x_off, pad_mode, padvals, out, ld_out, n_out, 0, 1, out_bias,
+                      stream);
+  PDD_REQUIRE(piece == 0 && x_off == 0 && out_bias == 0.f,
               "pdd_sweep_execute: the generic (sparse-grid) kernel reads channel-major input "
-              "at offset 0 only");
+              "at offset 0 without an output bias");
   // every staged index must stay inside int64 / the LDS image: the shifts are
   // bounded by the plan, the samples by N + n_out.
   const int64_t n_tblk = cdiv(n_out, p->v.TB());
@@ -1835,7 +1859,7 @@ int pdd_sweep_execute_grouped(const pdd_sweep_plan* p, const void* x, int64_t N,
               "pdd_sweep_execute_grouped: bad pad mode %d", pad_mode);
   if (n_out == 0) return 0;
   return execute_il(p, x, N, InLayout{ld, 0, 0, 0}, 0, pad_mode, padvals, out, ld_out, n_out, row_g,
-                    row_d, stream);
+                    row_d, 0.f, stream);
 }
 
 int pdd_sweep_set_timing(pdd_sweep_plan* p, int on) {

@@ -1,6 +1,22 @@
 """Streaming FRB-style pipeline (BASELINE.json configs[4]; SURVEY.md §8(d)
-config 5): continuous filterbank blocks -> zero-DM (float mode) -> downsample
--> batched DM sweep, with pinned-host H2D copies overlapped with compute.
+config 5): continuous filterbank blocks -> zero-DM -> downsample -> batched DM
+sweep, with pinned-host H2D copies overlapped with compute.
+
+Zero-DM modes (bin/zero_dm_filter.py:30-39 subtracts each spectrum's channel
+mean; for integer data the mean is rounded half-to-even and the difference is
+taken in the data dtype):
+  * ``"auto"`` (default): ``"int"`` where the exact path applies, else
+    ``"float"``.
+  * ``"int"`` (8-bit input, downsamp <= 2): x - round(mean) as an
+    exact signed integer (the reference's rounding without the uint8 wrap),
+    co-added and offset into 16-bit samples <= 1023 (pdd_zdm_int_downsample)
+    so the exact packed-u16 sweep runs; the plane bias is removed in the
+    sweep epilogue.  Every plane value is an exact integer.
+  * ``"wrap"``: the reference's uint8 result, (x - round(mean)) mod 256, on
+    the same exact 16-bit path (downsamp <= 4).
+  * ``"float"`` (``True``): x - mean in float32, then the float32 sweep
+    (the reference's semantics for float data).
+  * ``False``: no filter (8-bit input, downsamp <= 4: exact 16-bit path).
 
 Per input chunk (``block`` spectra of the stream, time-major [n, nchan] in
 file order, 8/16-bit or float32):
@@ -8,7 +24,7 @@ file order, 8/16-bit or float32):
     copy stream : pinned chunk i --H2D--> raw[i % 3][0:ov]      (head, event)
                   pinned chunk i --H2D--> raw[i % 3][ov:n]     (rest, event)
     compute     : raw[(i-1) % 3][block : block + ov] <- raw[i % 3][0 : ov]   (D2D)
-                  pdd_zdm_downsample(raw[(i-1) % 3])  -> [C, (block + ov)/ds] f32
+                  prologue(raw[(i-1) % 3])  -> [C, (block + ov)/ds] u16 (or f32)
                   DMSweep (interleave + sweep, trim)   -> plane [D, block/ds]
 
 ``ov = max_bin * ds`` input spectra (the largest dispersion delay of the grid
@@ -33,12 +49,29 @@ from .sweep import DMSweep
 _CODES = {torch.uint8: _lib.U8, torch.int16: _lib.U16, torch.float32: _lib.F32}
 
 
+_ZDM = {"none": _lib.ZDM_NONE, "int": _lib.ZDM_INT, "wrap": _lib.ZDM_WRAP}
+
+
+def prologue(raw, n, C, ds, mode, img, offset=0, stream=None):
+    """zero-DM (``mode``) + downsample by ``ds`` + corner turn of the
+    time-major block raw[:n] into the channel-major image ``img``: 16-bit
+    offset integers (pdd_zdm_int_downsample) when ``img`` is int16, float32
+    (pdd_zdm_downsample) otherwise."""
+    if img.dtype == torch.int16:
+        call("pdd_zdm_int_downsample", ptr(raw), _lib.U8, n, C, raw.stride(0), ds, _ZDM[mode],
+             offset, ptr(img), img.stride(0), stream_ptr(stream))
+    else:
+        call("pdd_zdm_downsample", ptr(raw), _CODES[raw.dtype], n, C, raw.stride(0), ds,
+             int(mode != "none"), ptr(img), img.stride(0), stream_ptr(stream))
+    return img
+
+
 class StreamingSweep(object):
     """``StreamingSweep(dms, freqs, dt)(chunks)`` yields ``(t0, plane)``:
     plane columns t0 .. t0 + plane.shape[1] - 1 of the stream's DM-time plane
     (downsampled time index)."""
 
-    def __init__(self, dms, freqs, dt, block=1 << 18, downsamp=2, zero_dm=True,
+    def __init__(self, dms, freqs, dt, block=1 << 18, downsamp=2, zero_dm="auto",
                  dtype=torch.uint8, device="cuda"):
         _lib.require_gpu()
         assert block % downsamp == 0 and 64 % downsamp == 0
@@ -46,10 +79,23 @@ class StreamingSweep(object):
         self.C = len(self.freqs)
         self.ds = int(downsamp)
         self.dt = dt
-        self.zero_dm = bool(zero_dm)
+        mode = {True: "float", False: "none"}.get(zero_dm, zero_dm)
+        if mode == "auto":
+            mode = "int" if (dtype == torch.uint8 and self.C % 16 == 0 and self.ds <= 2) else "float"
+        if mode not in ("int", "wrap", "float", "none"):
+            raise ValueError("zero_dm must be 'auto', 'int', 'wrap', 'float', True or False")
         self.dtype = dtype
         self.device = torch.device(device)
-        self.sweep = DMSweep(dms, self.freqs, dt * self.ds, dtype="f32")
+        # the exact 16-bit path: 8-bit input, 16-B rows, co-added values <= 1023
+        self.exact = (dtype == torch.uint8 and mode != "float" and self.C % 16 == 0
+                      and self.ds <= (2 if mode == "int" else 4))
+        if mode in ("int", "wrap") and not self.exact:
+            raise ValueError("zero_dm=%r needs 8-bit input, nchan %% 16 == 0 and downsamp <= %d"
+                             % (mode, 2 if mode == "int" else 4))
+        self.mode = mode
+        self.zero_dm = mode != "none"
+        self.offset = 255 * self.ds if mode == "int" else 0
+        self.sweep = DMSweep(dms, self.freqs, dt * self.ds, dtype="u16" if self.exact else "f32")
         self.D = self.sweep.D
         self.max_bin = max(0, self.sweep.max_bin)
         self.block = int(block)
@@ -59,7 +105,9 @@ class StreamingSweep(object):
         self.nbuf = 3
         self.raw = [torch.empty((n_raw, self.C), dtype=dtype, device=self.device)
                     for _ in range(self.nbuf)]
-        self.f32 = torch.empty((self.C, n_raw // self.ds), dtype=torch.float32, device=self.device)
+        self.img = torch.empty((self.C, n_raw // self.ds),
+                               dtype=torch.int16 if self.exact else torch.float32,
+                               device=self.device)
         self.copy_stream = torch.cuda.Stream(device=self.device)
         self.h2d_head = [torch.cuda.Event() for _ in range(self.nbuf)]
         self.h2d = [torch.cuda.Event() for _ in range(self.nbuf)]
@@ -79,9 +127,8 @@ class StreamingSweep(object):
             out = torch.empty((self.D, max(n_out, 0)), dtype=torch.float32, device=self.device)
         if n_out == 0:
             return out[:, :0]
-        call("pdd_zdm_downsample", ptr(raw), _CODES[self.dtype], n_valid, self.C, raw.stride(0),
-             self.ds, int(self.zero_dm), ptr(self.f32), self.f32.stride(0), stream_ptr())
-        self.sweep(self.f32[:, :nd], trim=True, out=out)
+        prologue(raw, n_valid, self.C, self.ds, self.mode, self.img, self.offset)
+        self.sweep(self.img[:, :nd], trim=True, out=out, out_bias=-float(self.offset * self.C))
         return out[:, :n_out]
 
     def __call__(self, chunks, planes=None):

@@ -19,6 +19,12 @@ from ._lib import call, ptr, stream_ptr
 from . import delays as _delays
 
 
+# 16-bit sweep input: int16 storage (values 0..1023 have the same bits) or
+# torch.uint16 where this torch has it
+_U16_TYPES = tuple(t for t in (torch.int16, getattr(torch, "uint16", None)) if t is not None)
+_CODE_OF = {"f32": _lib.F32, "u8": _lib.U8, "u16": _lib.U16}
+
+
 def _is_int_pad(padval):
     if isinstance(padval, str):
         return padval == "rotate"
@@ -28,8 +34,10 @@ def _is_int_pad(padval):
 class DMSweep(object):
     """A reusable sweep plan: ``DMSweep(dms, freqs, dt)(x)`` -> device plane.
 
-    dtype: 'f32' (float32 input) or 'u8' (8-bit filterbank input; exact
-    integer accumulation).  ``x`` is a [C, N] device tensor of that dtype or
+    dtype: 'f32' (float32 input), 'u8' (8-bit filterbank input; exact
+    integer accumulation) or 'u16' (16-bit samples <= 1023, e.g. the offset
+    integer zero-DM + downsample prologue of the stream; exact).  ``x`` is a
+    [C, N] device tensor of that dtype (int16 / uint16 storage for 'u16') or
     a ``Spectra``."""
 
     def __init__(self, dms, freqs, dt, cur_dm=0.0, dtype="f32"):
@@ -71,14 +79,16 @@ class DMSweep(object):
             return max(0, N - self.max_bin)
         return N
 
-    def __call__(self, x, padval=0, trim=True, out=None, stream=None, n_out=None):
+    def __call__(self, x, padval=0, trim=True, out=None, stream=None, n_out=None, out_bias=0.0):
         """Sweep ``x`` into ``out`` (allocated if None).  ``n_out`` (optional)
         is the number of plane columns to produce; the default is this grid's
         trimmed width ``n_out(N, trim)``.  A caller sweeping a slice of a
         larger grid passes the GLOBAL width (<= this slice's), so every rank
         of a DM-sharded sweep fills identically shaped rows; columns past a
         row's own trimmed length are the reference's padded values
-        (dedisperse(trim=False) semantics), never out-of-bounds reads."""
+        (dedisperse(trim=False) semantics), never out-of-bounds reads.
+        ``out_bias`` is added to every plane value (an offset encoding of the
+        input, e.g. -offset * C for the u16 prologue; exact for integers)."""
         from .formats.spectra import Spectra, _pad_args
         f32 = None
         if isinstance(x, Spectra):
@@ -118,13 +128,24 @@ class DMSweep(object):
             else:
                 mode = _lib.PAD_VALUE
                 pv = torch.full((self.C,), float(padval), dtype=torch.float32, device=x.device)
+        elif x.dtype in _U16_TYPES:
+            code = _lib.U16
+            if isinstance(padval, str):
+                if padval != "rotate":
+                    raise ValueError("16-bit sweep input takes integer or 'rotate' pads")
+                mode, pv = _lib.PAD_ROTATE, None
+            else:
+                if not (float(padval).is_integer() and 0 <= float(padval) <= 1023):
+                    raise ValueError("16-bit sweep pads must be integers in [0, 1023]")
+                mode = _lib.PAD_VALUE
+                pv = torch.full((self.C,), float(padval), dtype=torch.float32, device=x.device)
         elif x.dtype == torch.float32:
             code = _lib.F32
             mode, pv = _pad_args(x, padval)
         else:
-            raise TypeError("sweep input must be float32 or uint8")
-        call("pdd_sweep_execute", self._plan(code), ptr(x), N, x.stride(0), mode, ptr(pv),
-             ptr(out), out.stride(0), n_out, stream_ptr(stream))
+            raise TypeError("sweep input must be float32, uint8 or 16-bit")
+        call("pdd_sweep_execute_ex", self._plan(code), ptr(x), N, x.stride(0), 0, 0, mode, ptr(pv),
+             ptr(out), out.stride(0), n_out, float(out_bias), stream_ptr(stream))
         return out
 
     def sweep_pieces(self, xp, N, piece, x_off, n_out, out, stream=None):
@@ -141,13 +162,13 @@ class DMSweep(object):
         assert xp.is_contiguous() and xp.numel() >= -(-N // piece) * self.C * piece
         pv = torch.zeros(self.C, dtype=torch.float32, device=xp.device)
         call("pdd_sweep_execute_ex", self._plan(code), ptr(xp), N, 0, piece, x_off, _lib.PAD_VALUE,
-             ptr(pv), ptr(out), out.stride(0), n_out, stream_ptr(stream))
+             ptr(pv), ptr(out), out.stride(0), n_out, 0.0, stream_ptr(stream))
         return out
 
     def set_timing(self, on=True, code=None):
         """Bracket the sweep kernel of every execute with HIP events (on the
         execute stream); read the last duration with kernel_ms()."""
-        code = (_lib.U8 if self.dtype == "u8" else _lib.F32) if code is None else code
+        code = _CODE_OF[self.dtype] if code is None else code
         _lib.check(_lib.lib().pdd_sweep_set_timing(self._plan(code), int(bool(on))),
                    "pdd_sweep_set_timing")
         self._timed_code = code
@@ -222,7 +243,7 @@ class GroupedSweep(object):
         self.n_grp, self.D, self.C = t.shape
         self.max_bin = int(t.max()) if t.size else 0
         self.dtype = dtype
-        code = _lib.U8 if dtype == "u8" else _lib.F32
+        code = _CODE_OF[dtype]
         h = ctypes.c_void_p()
         _lib.check(_lib.lib().pdd_sweep_plan_create_grouped(
             t.ctypes.data_as(ctypes.c_void_p), self.n_grp, self.D, self.C, code, ctypes.byref(h)),

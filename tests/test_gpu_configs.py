@@ -11,7 +11,8 @@
   at the full 2^22 length the size-independent properties (u8 plane == f32
   plane, rows == the independent single-DM kernel, sharded == direct);
 * configs[4]: the 4096-channel 2048-DM stream of 2^18-spectrum blocks equals
-  the one-shot zero-DM + downsample + sweep, bit for bit.
+  the one-shot zero-DM + downsample + sweep, bit for bit (integer zero-DM on
+  the exact 16-bit path, also against oracle rows; and the float mode).
 
 All inputs are integer-valued 8-bit data with integer pads, so every
 comparison is bit-exact (float32 sums of integers < 2^24), except pad 'mean'
@@ -166,30 +167,52 @@ def test_config3_full_length_properties(gpu):
     sub.close()
 
 
-def test_config4_stream_equals_one_shot(gpu):
-    """configs[4]: 4096-ch 8-bit blocks of 2^18 spectra, zero-DM (float) +
-    downsample 2 + 2048-DM sweep, streamed from pinned host memory ==
-    the one-shot pipeline over the whole stream."""
+@pytest.mark.parametrize("zdm", ["int", "float"])
+def test_config4_stream_equals_one_shot(gpu, zdm):
+    """configs[4]: 4096-ch 8-bit blocks of 2^18 spectra, zero-DM + downsample
+    2 + 2048-DM sweep, streamed from pinned host memory == the one-shot
+    pipeline over the whole stream.  'int' (the default): the exact 16-bit
+    path, also checked bit for bit against the oracle on a window of rows;
+    'float': the float32 path."""
     import torch
     from pypulsar_amd import _lib
     from pypulsar_amd._lib import call, ptr, stream_ptr
-    from pypulsar_amd.stream import StreamingSweep
+    from oracle import spectra_oracle as orc
+    from pypulsar_amd.stream import StreamingSweep, prologue
     from pypulsar_amd.sweep import DMSweep
     C, D, block, ds = 4096, 2048, 1 << 18, 2
     freqs = band(C)
     dms = np.linspace(0.0, 1000.0, D)
     N = 3 * block + 100000
     x = np.random.default_rng(13).integers(0, 256, size=(N, C), dtype=np.uint8)
-    st = StreamingSweep(dms, freqs, DT, block=block, downsamp=ds)
-    assert st.ov == 7252 * ds
+    st = StreamingSweep(dms, freqs, DT, block=block, downsamp=ds, zero_dm=zdm)
+    assert st.ov == 7252 * ds and st.exact == (zdm == "int")
     chunks = [torch.from_numpy(x[i:i + block]).pin_memory() for i in range(0, N, block)]
     parts = [p.clone() for _, p in st(chunks)]
     st.close()
     got = torch.cat(parts, dim=1)
     xd = torch.from_numpy(x).cuda()
-    f32 = torch.empty((C, N // ds), dtype=torch.float32, device="cuda")
-    call("pdd_zdm_downsample", ptr(xd), _lib.U8, N, C, C, ds, 1, ptr(f32), f32.stride(0),
-         stream_ptr())
-    want = DMSweep(dms, freqs, DT * ds)(f32)
+    if zdm == "int":
+        img = torch.empty((C, N // ds), dtype=torch.int16, device="cuda")
+        prologue(xd, N, C, ds, "int", img, 255 * ds)
+        sw = DMSweep(dms, freqs, DT * ds, dtype="u16")
+        want = sw(img, out_bias=-255.0 * ds * C)
+    else:
+        f32 = torch.empty((C, N // ds), dtype=torch.float32, device="cuda")
+        call("pdd_zdm_downsample", ptr(xd), _lib.U8, N, C, C, ds, 1, ptr(f32), f32.stride(0),
+             stream_ptr())
+        sw = DMSweep(dms, freqs, DT * ds)
+        want = sw(f32)
     assert got.shape == want.shape
     assert torch.equal(got, want)
+    if zdm == "int":
+        # oracle window: plane columns [j0, j0 + W) need input spectra
+        # [j0 ds, (j0 + W + max_bin) ds) -- across the seam of blocks 1 and 2
+        W, mb = 2048, sw.max_bin
+        j0 = block // ds - 1000
+        win = x[j0 * ds:(j0 + W + mb) * ds]
+        ref_img = orc.zdm_int_downsample(win, ds, "int")
+        rows = [0, 1, 777, 1500, 2047]
+        ref = orc.sweep_rows_inside(ref_img, sw.table[rows], W)
+        np.testing.assert_array_equal(got[rows, j0:j0 + W].cpu().numpy(), ref)
+    sw.close()

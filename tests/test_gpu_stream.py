@@ -35,8 +35,51 @@ def test_zdm_downsample(gpu, dtype, factor, zdm):
         assert rel_err(got, want) <= 1e-5
 
 
-@pytest.mark.parametrize("nchunks,last", [(3, 4096), (4, 1000)])
-def test_stream_equals_one_shot(gpu, nchunks, last):
+@pytest.mark.parametrize("mode,factor", [("int", 1), ("int", 2), ("wrap", 2), ("wrap", 4),
+                                         ("none", 4)])
+def test_zdm_int_downsample(gpu, mode, factor):
+    """Integer prologue of the exact 16-bit stream path, bit-exact against the
+    oracle (incl. the reference's uint8 wrap, zero_dm_filter.py:30-39)."""
+    import torch
+    from pypulsar_amd import _lib
+    from pypulsar_amd.stream import prologue
+    nspec, C = 1000 + factor - 1, 96
+    x = u8_data(nspec, C, 7)
+    x[:5] = 255   # extreme spectra: differences at +-255
+    x[5:9, :48] = 0
+    x[9] = np.arange(C) % 2 * 255  # mean 127.5: the half-to-even tie
+    xd = torch.from_numpy(x).cuda()
+    img = torch.full((C, nspec // factor + 3), -1, dtype=torch.int16, device="cuda")
+    off = 255 * factor if mode == "int" else 0
+    prologue(xd, nspec, C, factor, mode, img, off)
+    got = img.cpu().numpy().astype(np.int64) & 0xffff
+    want = orc.zdm_int_downsample(x, factor, mode) + off
+    np.testing.assert_array_equal(got[:, :nspec // factor], want)
+    assert (got[:, nspec // factor:] == 0xffff).all()  # nothing past n_out written
+
+
+def test_sweep_u16_with_bias(gpu):
+    """16-bit sweep input (values <= 1023, the 64-channel flush) and the
+    epilogue bias: bit-exact against the oracle plane."""
+    import torch
+    from pypulsar_amd.sweep import DMSweep
+    C, N = 200, 6000
+    freqs = band(C)
+    rng = np.random.default_rng(11)
+    x = rng.integers(0, 1024, (C, N)).astype(np.int16)
+    x[:, :50] = 1023  # carries would show at the maximum
+    dms = np.linspace(0.0, 150.0, 50)
+    sw = DMSweep(dms, freqs, DT, dtype="u16")
+    got = sw(torch.from_numpy(x).cuda(), out_bias=-1000.0 * C).cpu().numpy()
+    want = orc.sweep_plane(x.astype(np.float64), orc.sweep_table(dms, freqs, DT)) - 1000.0 * C
+    np.testing.assert_array_equal(got, want)
+    sw.close()
+
+
+@pytest.mark.parametrize("nchunks,last,zdm", [(3, 4096, "float"), (4, 1000, "float"),
+                                             (3, 4096, "int"), (4, 1000, "int"),
+                                             (3, 1000, "wrap")])
+def test_stream_equals_one_shot(gpu, nchunks, last, zdm):
     import torch
     from pypulsar_amd.stream import StreamingSweep
     from pypulsar_amd.sweep import DMSweep
@@ -45,12 +88,21 @@ def test_stream_equals_one_shot(gpu, nchunks, last):
     dms = np.linspace(0.0, 200.0, 40)  # max delay 2900 input spectra < block
     N = block * (nchunks - 1) + last
     x = u8_data(N, C, 17)  # [time, chan], file order
-    st = StreamingSweep(dms, freqs, DT, block=block, downsamp=ds)
+    st = StreamingSweep(dms, freqs, DT, block=block, downsamp=ds, zero_dm=zdm)
+    assert st.exact == (zdm != "float")
     chunks = [torch.from_numpy(x[i:i + block]).pin_memory() for i in range(0, N, block)]
     parts = [(t0, p.cpu().numpy()) for t0, p in st(chunks)]
     torch.cuda.synchronize()
     got = np.concatenate([p for _, p in parts], axis=1)
     assert [t0 for t0, _ in parts] == list(np.cumsum([0] + [p.shape[1] for _, p in parts[:-1]]))
+    if zdm != "float":
+        # exact integer path: the oracle composition bit for bit
+        ref = orc.sweep_plane(orc.zdm_int_downsample(x, ds, zdm).astype(np.float64),
+                              orc.sweep_table(dms, freqs, DT * ds))
+        assert got.shape == ref.shape
+        np.testing.assert_array_equal(got, ref)
+        st.close()
+        return
     # one-shot on the device: same prologue + sweep over the whole stream
     from pypulsar_amd import _lib
     from pypulsar_amd._lib import call, ptr, stream_ptr
