@@ -8,7 +8,9 @@ trim=True) -> downsample -> scaled -> smooth -> plot, with every step a HIP
 kernel and only the final 2-D image and summed series copied to the host.
 
 Differences from the reference, all where it cannot run:
-  * ``--mask`` needs PRESTO's rfifind (absent): it raises a clear error;
+  * ``--mask`` reads the rfifind ``.mask`` file with
+    pypulsar_amd.formats.rfifind (a restatement of PRESTO's format; PRESTO is
+    absent) and masks on the device (Spectra.masked, 'median-mid80');
     ``.fits`` input goes through pypulsar_amd.formats.psrfits (device decode);
   * with dm == 0 the reference's ``dmtime`` is unbound (waterfaller.py:193-196):
     here it is 0;
@@ -46,9 +48,13 @@ def get_data(rawdatafile, start, duration=None, nbins=None, mask=None):
         if duration is None:
             raise ValueError("At least one of 'duration' and 'nbins' must be provided!")
         nbins = int(np.round(duration / rawdatafile.tsamp))
+    data = rawdatafile.get_spectra(start_bin, nbins)
     if mask is not None:
-        raise ValueError("--mask needs PRESTO's rfifind, which is not available")
-    return rawdatafile.get_spectra(start_bin, nbins)
+        from pypulsar_amd.formats import rfifind
+        rfimask = mask if isinstance(mask, rfifind.rfifind) else rfifind.rfifind(mask)
+        datamask = rfifind.get_mask(rfimask, start_bin, nbins)
+        data = data.masked(datamask, maskval="median-mid80")
+    return data
 
 
 def prepare_data(data, smooth=1, downsamp=1, dm=0, nsub=None, subdm=None, scaleindep=False,

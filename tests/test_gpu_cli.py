@@ -98,6 +98,43 @@ def test_waterfaller_cli(gpu, tmp_path):
     assert rel_err(data.data, d) <= 1e-5
 
 
+def test_waterfaller_mask(gpu, tmp_path):
+    """--mask: the rfifind mask of the span (get_mask, waterfaller.py:28-48)
+    applied with masked(..., 'median-mid80') before the chain
+    (waterfaller.py:92-99), against the oracle composition."""
+    from pypulsar_amd.bin import waterfaller as w
+    from pypulsar_amd.formats import filterbank as fbm
+    from pypulsar_amd.formats import rfifind as rf
+    C, N, ppi = 64, 12000, 1000
+    x = u8_data(C, N, 21)
+    fn = _fil(tmp_path, x.T.copy())
+    rng = np.random.default_rng(5)
+    per = [np.sort(rng.choice(C, size=int(rng.integers(0, 12)), replace=False))
+           for _ in range(N // ppi)]
+    per[3] = np.arange(C)  # a fully zapped interval
+    mfn = str(tmp_path / "in_rfifind.mask")
+    rf.write_mask(mfn, C, ppi, per)
+    png = str(tmp_path / "wf.png")
+    assert w.main(["-T", "0.01", "-n", "3000", "-d", "150", "-s", "16", "--mask", mfn,
+                   "--outfile", png, fn]) == 0
+    opts = type("O", (), dict(dm=150.0, start=0.01, duration=None, nbins=3000, maskfile=mfn,
+                              width_bins=1, downsamp=1, nsub=16, subdm=150.0, scaleindep=False))
+    data = w.run(fn, opts)
+    fb = fbm.filterbank(fn)
+    start = int(np.round(0.01 / DT))
+    nb = 3000 + int(np.round(orc.delay_from_DM(150.0, fb.freqs.min()) / DT))
+    d = x[:, start:start + nb].astype(np.float64)
+    mask = np.zeros_like(d, dtype=bool)
+    for j in range(nb):
+        mask[per[(start + j) // ppi], j] = True
+    d = orc.masked(d, mask, "median-mid80")
+    d, f = orc.subband(d, fb.freqs, DT, 16, 150.0, padval="mean")
+    d, _ = orc.dedisperse(d, f, DT, 150.0, padval="mean", trim=True)
+    d = orc.scaled(d)
+    assert data.data.shape == d.shape
+    assert rel_err(data.data, d) <= 1e-5
+
+
 def test_waterfaller_psrfits(gpu, tmp_path):
     """waterfaller.py on a PSRFITS file (waterfaller.py:58-59 opens .fits with
     psrfits.PsrfitsFile): same pipeline result as on a filterbank holding the
