@@ -20,7 +20,7 @@ SRC = os.path.join(ROOT, "gpurun_out", "prof_r2")
 DST = os.path.join(ROOT, "profiles")
 TAG = sys.argv[1] if len(sys.argv) > 1 else "r2"
 ARGS = {"config3": "--config config3", "config2_u8": "--config config2 --dtype u8",
-        "config2_f32": "--config config2 --dtype f32"}
+        "config2_f32": "--config config2 --dtype f32", "stream": "--config stream"}
 
 
 def per_kernel(pattern, counter):
