@@ -565,7 +565,8 @@ __device__ __forceinline__ int stage_il_dma(uint32_t lds_dst, const float4* src,
 // reads and returns out of order, so every counted LDS wait became
 // lgkmcnt(0): f32 43 -> 62 ms.)
 // Metadata: mt[dblk][c][ROW], ROW = DB + 4: the tile's DB shifts at channel c
-// relative to their minimum bmin, then {bmin, span, 0, 0}.  Loader 0 DMAs
+// relative to their minimum bmin, as byte offsets into the channel's LDS
+// image (16 x elements), then {bmin, span, 0, 0} (in elements).  Loader 0 DMAs
 // the rows of chunk j into ONE shared ring (slot j % MR) MA = 2(NBUF-1)
 // chunks ahead, before the samples of chunk j - MA + NBUF - 1; its counted
 // vmcnt before barrier k therefore also retires the rows of chunk
@@ -630,6 +631,11 @@ __device__ __forceinline__ void il_tile_of(int bid, int n_tblk, int n_dblk, int 
   tblk = x * TX + band * GT + r / gj;
 }
 
+// a + b + c: one v_add3_u32 (two packed-u16 sample adds per lane)
+__device__ __forceinline__ uint32_t add3_u32(uint32_t a, uint32_t b, uint32_t c) {
+  return a + b + c;
+}
+
 template <int G, int DPW, int NCW, int NLW, int CC, int NBUF, bool U16 = false>
 __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const float4* __restrict__ R0, int64_t nR, int C, int lo, const int* __restrict__ mt,
@@ -646,7 +652,8 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   constexpr int SLOT = il_slot(CC, DB);
   constexpr int MA = il_ma(NBUF), MR = il_mr(NBUF);
   constexpr int S = U16 ? 8 : 4;  // samples per 16-byte element (quarters / eighths)
-  static_assert(DPW == 4 && G == (U16 ? 2 : 4), "b128 shift reads; one trial = 4 (f32) or 2 (u16) groups");
+  static_assert(DPW == 4 && G == (U16 ? 2 : 4) && DPW * CC <= 64,
+                "4 trials per wave, 4 (f32) or 2 (u16) groups; one lane per (channel, trial)");
   static_assert(NBUF >= 2 && MA >= 2 * NBUF - 2 && MR > MA, "ring geometry");
   extern __shared__ __attribute__((aligned(16))) float smf[];
   uint4* img = reinterpret_cast<uint4*>(smf);
@@ -758,13 +765,14 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   // accumulators as float pairs: the adds issue as v_pk_add_f32 (two samples
   // per VALU instruction: half the issue slots of scalar v_add_f32)
   typedef float f32x2_t __attribute__((ext_vector_type(2)));
-  f32x2_t acc[DPW][G][S / 2];
+  constexpr int AJ = DPW, AG = G, AH = S / 2;
+  f32x2_t acc[AJ][AG][AH];
 #pragma unroll
-  for (int j = 0; j < DPW; ++j)
+  for (int j = 0; j < AJ; ++j)
 #pragma unroll
-    for (int g = 0; g < G; ++g)
+    for (int g = 0; g < AG; ++g)
 #pragma unroll
-      for (int h = 0; h < S / 2; ++h) acc[j][g][h] = (f32x2_t){0.f, 0.f};
+      for (int h = 0; h < AH; ++h) acc[j][g][h] = (f32x2_t){0.f, 0.f};
   uint32_t a16[U16 ? DPW : 1][U16 ? G : 1][4];
   if constexpr (U16) {
 #pragma unroll
@@ -791,8 +799,8 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   const uint32_t lane_byte = lds_addr_of(img) + lane * 16;
   const uint32_t meta_base = lds_addr_of(metar) + w * DPW * 4;  // loader 0's ring
   typedef int i32x4_t __attribute__((ext_vector_type(4)));
-  typedef __attribute__((address_space(3))) i32x4_t lds_i32x4_t;
   typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+  static_assert(!U16 || DPW * CC <= 64, "one lane per (channel, trial) shift");
   typedef __attribute__((address_space(3))) u32x4_t lds_u32x4_t;
   uint64_t ts_poll = 0, ts_comp = 0, tA = 0, tB = 0;
   __builtin_amdgcn_s_barrier();  // prologue barrier (metadata landed)
@@ -809,26 +817,34 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     if (stamps) { tB = __builtin_amdgcn_s_memtime(); ts_poll += tB - tA; }
     const int slot = k % MR;
     const int ncc = min(CC, C - k * CC);
+    // ONE ds_read_b32 brings the wave's DPW shifts of all CC channels of the
+    // chunk (lane DPW*i + j = trial j at channel i, as LDS byte offsets: the
+    // plan stores them pre-scaled by 16), each broadcast by v_readlane when
+    // its reads issue.  (A ds_read_b128 of 4 shifts per channel costs 4 LDS
+    // cycles per channel; this costs 2 per chunk plus one VALU per shift:
+    // configs[3] u8 288 -> 280 ms, configs[1] u8 32.7 -> 27.3 ms.)
+    const int ml = min(lane / DPW, CC - 1) * ROW + lane % DPW;
+    const int vmeta = *(const __attribute__((address_space(3))) int*)(uintptr_t)(
+        meta_base + (uint32_t)((slot * SLOT + ml) * 4));
+    auto chan_base = [&](int i) -> uint32_t {
+      return lane_byte + (uint32_t)((b * CC + i) * stride * 16);
+    };
     if (!(dbg & 2)) {
-#pragma unroll
-      for (int i = 0; i < CC; ++i) {
-        if (i >= ncc) break;
-        const i32x4_t o =
-            *(const lds_i32x4_t*)(uintptr_t)(meta_base + (uint32_t)((slot * SLOT + i * ROW) * 4));
-        const int ov[4] = {o.x, o.y, o.z, o.w};
-        const uint32_t cb = lane_byte + (uint32_t)((b * CC + i) * stride * 16);
-        if constexpr (U16) {
-          // two trials at a time (a full scheduling barrier between the
-          // halves keeps the live read registers within the 128-VGPR budget)
+      if constexpr (U16) {
+        // one channel: two trials at a time (a full scheduling barrier
+        // between the halves keeps the live read registers within budget)
+        auto one16 = [&](int i) {
+          const uint32_t cb = chan_base(i);
 #pragma unroll
           for (int jh = 0; jh < DPW; jh += 2) {
             u32x4_t v[2][G];
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+            for (int j = 0; j < 2; ++j) {
+              const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane(vmeta, DPW * i + jh + j);
 #pragma unroll
               for (int g2 = 0; g2 < G; ++g2)
-                v[j][g2] =
-                    *(const lds_u32x4_t*)(uintptr_t)(cb + (uint32_t)(ov[jh + j] * 16) + g2 * 1024);
+                v[j][g2] = *(const lds_u32x4_t*)(uintptr_t)(cb + sj + g2 * 1024);
+            }
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -840,17 +856,75 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
               }
             __builtin_amdgcn_sched_barrier(0);
           }
-          if (++since_flush == flush_n) {
-            since_flush = 0;
-            flush16();
+        };
+        // flush before a chunk could carry a u16 lane past 65535
+        if (since_flush + CC > flush_n) {
+          since_flush = 0;
+          flush16();
+        }
+        since_flush += CC;
+        // channel pairs pay on wide chunks; narrower ones (wide-span grids)
+        // measured faster one channel at a time
+        constexpr bool PAIRS = CC >= 8;
+        if (PAIRS && ncc == CC) {
+          // full chunk: channels in pairs (acc + x_c + x_c+1: one v_add3_u32
+          // per two samples), software-pipelined over the (pair, trial)
+          // steps: the reads of step s + PD issue before the adds of step s
+          constexpr int NS = (CC / 2) * DPW;
+          constexpr int PD = 1;  // steps in flight (deeper needs registers we lack)
+          u32x4_t v0[PD][G], v1[PD][G];
+          auto issue = [&](int st) {
+            const int i = 2 * (st / DPW), j = st % DPW;
+            const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane(vmeta, DPW * i + j);
+            const uint32_t s1 = (uint32_t)__builtin_amdgcn_readlane(vmeta, DPW * (i + 1) + j);
+            const uint32_t cb0 = chan_base(i), cb1 = chan_base(i + 1);
+#pragma unroll
+            for (int g2 = 0; g2 < G; ++g2) {
+              v0[st % PD][g2] = *(const lds_u32x4_t*)(uintptr_t)(cb0 + s0 + g2 * 1024);
+              v1[st % PD][g2] = *(const lds_u32x4_t*)(uintptr_t)(cb1 + s1 + g2 * 1024);
+            }
+          };
+          auto consume = [&](int st) {
+            const int j = st % DPW;
+#pragma unroll
+            for (int g2 = 0; g2 < G; ++g2) {
+              const u32x4_t x0 = v0[st % PD][g2], x1 = v1[st % PD][g2];
+              a16[j][g2][0] = add3_u32(a16[j][g2][0], x0.x, x1.x);
+              a16[j][g2][1] = add3_u32(a16[j][g2][1], x0.y, x1.y);
+              a16[j][g2][2] = add3_u32(a16[j][g2][2], x0.z, x1.z);
+              a16[j][g2][3] = add3_u32(a16[j][g2][3], x0.w, x1.w);
+            }
+          };
+#pragma unroll
+          for (int st = 0; st < PD - 1; ++st)
+            if (st < NS) issue(st);
+#pragma unroll
+          for (int st = 0; st < NS; ++st) {
+            if (st + PD - 1 < NS) issue(st + PD - 1);
+            consume(st);
+            __builtin_amdgcn_sched_barrier(0);
           }
+          if constexpr (CC & 1) one16(CC - 1);
         } else {
+#pragma unroll
+          for (int i = 0; i < CC; ++i) {
+            if (i >= ncc) break;
+            one16(i);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < CC; ++i) {
+          if (i >= ncc) break;
+          const uint32_t cb = chan_base(i);
           f32x4_t v[DPW][G];
 #pragma unroll
-          for (int j = 0; j < DPW; ++j)
+          for (int j = 0; j < DPW; ++j) {
+            const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane(vmeta, DPW * i + j);
 #pragma unroll
             for (int g2 = 0; g2 < G; ++g2)
-              v[j][g2] = *(const lds_f32x4_t*)(uintptr_t)(cb + (uint32_t)(ov[j] * 16) + g2 * 1024);
+              v[j][g2] = *(const lds_f32x4_t*)(uintptr_t)(cb + sj + g2 * 1024);
+          }
 #pragma unroll
           for (int j = 0; j < DPW; ++j)
 #pragma unroll
@@ -1675,6 +1749,9 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
     const Variant v = cands[vi];
     const bool il = v.kind == 0;
     if (n_grp > 1 && !il) continue;  // only the interleaved kernel sweeps groups
+    // the global-flush (DB 96) tilings flush every 256 channels (8-bit data
+    // only) and sweep whole chunks (C % CC == 0)
+    if (v.DPW == 8 && (dtype == PDD_U16 || C % v.CC != 0)) continue;
     if (dtype == PDD_U16 && !il) {     // the generic kernel reads 8-bit or float32 rows
       set_error("pdd_sweep_plan_create: DM grid too sparse for a 16-bit-input tile");
       return -1;
@@ -1721,7 +1798,8 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
       for (int64_t b = 0; b < n_dblk; ++b)
         for (int64_t c = 0; c < C; ++c) {
           const size_t base = off + (size_t)((b * C + c) * ROWN);
-          for (int64_t d = 0; d < DB; ++d) mt_all[base + d] = tab[(size_t)(c * Dpad + b * DB + d)];
+          // shifts as LDS byte offsets of the 16-B image elements
+          for (int64_t d = 0; d < DB; ++d) mt_all[base + d] = 16 * tab[(size_t)(c * Dpad + b * DB + d)];
           mt_all[base + DB] = bmin[(size_t)(b * C + c)];
           mt_all[base + DB + 1] = bspan[(size_t)(b * C + c)];
         }
