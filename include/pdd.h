@@ -93,6 +93,11 @@ int pdd_downsample(const float* x, int64_t C, int64_t N, int64_t ld, int64_t fac
  * bytes.  Used by the DDplan executor (spectra.py:329-351 per DDstep). */
 int pdd_downsample_u8(const uint8_t* x, int64_t C, int64_t N, int64_t ld, int64_t factor,
                       float* out, int64_t ld_out, void* stream);
+/* The same co-add kept as uint16 (factor 1..4: sums <= 1020), the input of
+ * the exact 16-bit sweep (PDD_U16) -- the DDplan executor's downsampled
+ * 8-bit steps (formats/spectra.py:329-351 on raw 8-bit rows). */
+int pdd_downsample_u8_u16(const uint8_t* x, int64_t C, int64_t N, int64_t ld, int64_t factor,
+                          uint16_t* out, int64_t ld_out, void* stream);
 
 /* Zero-DM filter: every spectrum minus its channel mean; integer data use
  * round-half-even of the float64 mean and wrap modulo 2^nbits, float32 data

@@ -34,7 +34,7 @@ EXPORTS = (
     "pdd_smooth", "pdd_zdm_downsample", "pdd_sweep_set_timing", "pdd_sweep_kernel_ms",
     "pdd_sweep_plan_create_grouped", "pdd_sweep_execute_grouped", "pdd_sp_chunk_stats",
     "pdd_sp_search", "pdd_psrfits_subints", "pdd_downsample_u8", "pdd_sweep_timing_read",
-    "pdd_sweep_execute_ex", "pdd_zdm_int_downsample",
+    "pdd_sweep_execute_ex", "pdd_zdm_int_downsample", "pdd_downsample_u8_u16",
 )
 
 
@@ -61,6 +61,7 @@ _SIGS = {
                             _int),
     "pdd_downsample": ([_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp], _int),
     "pdd_downsample_u8": ([_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp], _int),
+    "pdd_downsample_u8_u16": ([_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp], _int),
     "pdd_zero_dm": ([_vp, _int, _i64, _i64, _i64, _int, _vp, _i64, _vp], _int),
     "pdd_sweep_plan_create": ([_vp, _i64, _i64, _int, ctypes.POINTER(_vp)], _int),
     "pdd_sweep_execute": ([_vp, _vp, _i64, _i64, _int, _vp, _vp, _i64, _i64, _vp], _int),

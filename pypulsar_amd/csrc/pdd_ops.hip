@@ -339,9 +339,9 @@ __global__ __launch_bounds__(256) void k_downsample_v4(const float* __restrict__
 // 8-bit input (a Spectra's raw bytes): integer sums (exact), one 16-byte load
 // per lane when the factor divides 16 and the rows are 16-B aligned -- a
 // quarter of the float32 image's bytes (DDplan executor, spectra.py:329-351)
-template <int F>
+template <int F, typename OutT>
 __global__ __launch_bounds__(256) void k_downsample_u8v(const uint8_t* __restrict__ x, int64_t ld,
-                                                        int64_t nvec, float* __restrict__ out,
+                                                        int64_t nvec, OutT* __restrict__ out,
                                                         int64_t ld_out, int64_t nout,
                                                         int64_t tiles, bool vstore) {
   constexpr int PER = 16 / F;  // outputs per 16-byte vector
@@ -350,7 +350,7 @@ __global__ __launch_bounds__(256) void k_downsample_u8v(const uint8_t* __restric
   if (v >= nvec) return;
   const uint4 q = *reinterpret_cast<const uint4*>(x + c * ld + v * 16);
   const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-  float r[PER];
+  uint32_t r[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     uint32_t s = 0;
@@ -359,30 +359,45 @@ __global__ __launch_bounds__(256) void k_downsample_u8v(const uint8_t* __restric
       const int e = k * F + b;
       s += (w[e >> 2] >> (8 * (e & 3))) & 0xffu;
     }
-    r[k] = (float)s;
+    r[k] = s;
   }
-  float* o = out + c * ld_out + v * PER;
-  if constexpr (PER >= 4) {
-    if (vstore && v * PER + PER <= nout) {
+  OutT* o = out + c * ld_out + v * PER;
+  if constexpr (sizeof(OutT) == 4) {
+    if constexpr (PER >= 4) {
+      if (vstore && v * PER + PER <= nout) {
 #pragma unroll
-      for (int k = 0; k < PER; k += 4)
-        *reinterpret_cast<float4*>(o + k) = make_float4(r[k], r[k + 1], r[k + 2], r[k + 3]);
-      return;
+        for (int k = 0; k < PER; k += 4)
+          *reinterpret_cast<float4*>(o + k) =
+              make_float4((float)r[k], (float)r[k + 1], (float)r[k + 2], (float)r[k + 3]);
+        return;
+      }
+    } else if constexpr (PER == 2) {
+      if (vstore && v * PER + PER <= nout) {
+        *reinterpret_cast<float2*>(o) = make_float2((float)r[0], (float)r[1]);
+        return;
+      }
     }
-  } else if constexpr (PER == 2) {
-    if (vstore && v * PER + PER <= nout) {
-      *reinterpret_cast<float2*>(o) = make_float2(r[0], r[1]);
-      return;
+  } else {
+    // uint16 sums (F <= 4: <= 1020), packed two per dword
+    if constexpr (PER >= 4) {
+      if (vstore && v * PER + PER <= nout) {
+#pragma unroll
+        for (int k = 0; k < PER; k += 4)
+          *reinterpret_cast<uint2*>(o + k) = make_uint2(r[k] | (r[k + 1] << 16),
+                                                        r[k + 2] | (r[k + 3] << 16));
+        return;
+      }
     }
   }
 #pragma unroll
   for (int k = 0; k < PER; ++k)
-    if (v * PER + k < nout) o[k] = r[k];
+    if (v * PER + k < nout) o[k] = (OutT)r[k];
 }
 
+template <typename OutT>
 __global__ __launch_bounds__(256) void k_downsample_u8(const uint8_t* __restrict__ x, int64_t ld,
                                                        int64_t factor, int64_t nout,
-                                                       float* __restrict__ out, int64_t ld_out,
+                                                       OutT* __restrict__ out, int64_t ld_out,
                                                        int64_t tiles) {
   const int64_t c = blockIdx.x / tiles, tile = blockIdx.x % tiles;
   const int64_t j = tile * 256 + threadIdx.x;
@@ -390,7 +405,7 @@ __global__ __launch_bounds__(256) void k_downsample_u8(const uint8_t* __restrict
   const uint8_t* p = x + c * ld + j * factor;
   uint64_t s = 0;
   for (int64_t k = 0; k < factor; ++k) s += p[k];
-  out[c * ld_out + j] = (float)s;
+  out[c * ld_out + j] = (OutT)s;
 }
 
 // ---------------------------------------------------------------- zero-DM
@@ -1096,8 +1111,11 @@ int pdd_downsample(const float* x, int64_t C, int64_t N, int64_t ld, int64_t fac
   return 0;
 }
 
-int pdd_downsample_u8(const uint8_t* x, int64_t C, int64_t N, int64_t ld, int64_t factor,
-                      float* out, int64_t ld_out, void* stream) {
+}  // extern "C"
+
+template <typename OutT>
+static int downsample_u8(const uint8_t* x, int64_t C, int64_t N, int64_t ld, int64_t factor,
+                         OutT* out, int64_t ld_out, void* stream) {
   PDD_REQUIRE(x && out, "pdd_downsample_u8: null pointer");
   PDD_REQUIRE(factor >= 1 && C >= 0 && N >= 0 && ld >= N, "pdd_downsample_u8: bad shape");
   const int64_t nout = N / factor;
@@ -1111,9 +1129,12 @@ int pdd_downsample_u8(const uint8_t* x, int64_t C, int64_t N, int64_t ld, int64_
     const int64_t tiles = cdiv(nvec, 256);
     PDD_REQUIRE(C * tiles < (1ll << 31), "pdd_downsample_u8: too large");
     const int per = (int)(16 / factor);
-    const bool vstore = (uintptr_t)out % (per >= 4 ? 16 : 8) == 0 &&
-                        ld_out % (per >= 4 ? 4 : 2) == 0 && per >= 2;
-#define DV(F_) k_downsample_u8v<F_><<<(unsigned)(C * tiles), 256, 0, s>>>(x, ld, nvec, out, ld_out, nout, tiles, vstore)
+    const int64_t vb = sizeof(OutT) == 4 ? (per >= 4 ? 16 : 8) : 8;  // vector store bytes
+    const bool vstore = (uintptr_t)out % vb == 0 && (ld_out * (int64_t)sizeof(OutT)) % vb == 0 &&
+                        per >= (sizeof(OutT) == 4 ? 2 : 4);
+#define DV(F_)                                                                                 \
+  k_downsample_u8v<F_, OutT><<<(unsigned)(C * tiles), 256, 0, s>>>(x, ld, nvec, out, ld_out, nout, \
+                                                                   tiles, vstore)
     if (factor == 1) DV(1);
     else if (factor == 2) DV(2);
     else if (factor == 4) DV(4);
@@ -1123,10 +1144,24 @@ int pdd_downsample_u8(const uint8_t* x, int64_t C, int64_t N, int64_t ld, int64_
   } else {
     const int64_t tiles = cdiv(nout, 256);
     PDD_REQUIRE(C * tiles < (1ll << 31), "pdd_downsample_u8: too large");
-    k_downsample_u8<<<(unsigned)(C * tiles), 256, 0, s>>>(x, ld, factor, nout, out, ld_out, tiles);
+    k_downsample_u8<OutT><<<(unsigned)(C * tiles), 256, 0, s>>>(x, ld, factor, nout, out, ld_out,
+                                                               tiles);
   }
   PDD_LAUNCHED();
   return 0;
+}
+
+extern "C" {
+
+int pdd_downsample_u8(const uint8_t* x, int64_t C, int64_t N, int64_t ld, int64_t factor,
+                      float* out, int64_t ld_out, void* stream) {
+  return downsample_u8<float>(x, C, N, ld, factor, out, ld_out, stream);
+}
+
+int pdd_downsample_u8_u16(const uint8_t* x, int64_t C, int64_t N, int64_t ld, int64_t factor,
+                          uint16_t* out, int64_t ld_out, void* stream) {
+  PDD_REQUIRE(factor >= 1 && factor <= 4, "pdd_downsample_u8_u16: factor must be 1..4 (sums <= 1020)");
+  return downsample_u8<uint16_t>(x, C, N, ld, factor, out, ld_out, stream);
 }
 
 int pdd_zero_dm(const void* in, int dtype, int64_t nspec, int64_t nchan, int64_t ld, int layout,

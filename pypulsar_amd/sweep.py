@@ -31,6 +31,13 @@ def _is_int_pad(padval):
     return float(padval).is_integer() and 0 <= float(padval) <= 255
 
 
+def _is_int_pad16(padval):
+    """Pads the 16-bit sweep can bake in exactly (integers <= 1023, 'rotate')."""
+    if isinstance(padval, str):
+        return padval == "rotate"
+    return float(padval).is_integer() and 0 <= float(padval) <= 1023
+
+
 class DMSweep(object):
     """A reusable sweep plan: ``DMSweep(dms, freqs, dt)(x)`` -> device plane.
 
@@ -317,14 +324,18 @@ class DDplanExecutor(object):
             s.ds = int(step.downsamp)
             s.dt = dt * s.ds
             s.n_ds = self.N // s.ds if s.ds > 1 else self.N
-            s.x = (torch.empty((self.C, s.n_ds), dtype=torch.float32, device=self.device)
-                   if s.ds > 1 else None)
+            # 8-bit rows downsampled by <= 4 stay exact integers <= 1020: the
+            # co-add is kept as uint16 and swept on the 16-bit path
+            s.u16 = bool(raw8) and 1 < s.ds <= 4
+            s.x = None      # float32 image of a downsampled step (allocated on use)
+            s.x16 = (torch.empty((self.C, s.n_ds), dtype=torch.int16, device=self.device)
+                     if s.u16 else None)
             calls = step.subband_calls()
             s.two_stage = calls[0][0] is not None
             if not s.two_stage:
                 # 8-bit rows at full rate go through the exact u16 sweep
                 s.sw = DMSweep(step.DMs, self.freqs, s.dt, cur_dm=cur_dm,
-                               dtype="u8" if (raw8 and s.ds == 1) else "f32")
+                               dtype="u8" if (raw8 and s.ds == 1) else ("u16" if s.u16 else "f32"))
                 s.n_out = s.sw.n_out(s.n_ds, True)
                 s.plane = torch.empty((s.sw.D, max(s.n_out, 1)), dtype=torch.float32,
                                       device=self.device)
@@ -337,8 +348,8 @@ class DDplanExecutor(object):
             # stage 1: [nsub groups][ncall trials][cps channels]
             t1 = np.stack([_delays.subband_bins(sd, self.freqs, s.dt, nsub, cur_dm=cur_dm)
                            for sd in subdms])                      # [ncall, C]
-            t1 = t1.reshape(ncall, nsub, cps).transpose(1, 0, 2)    # [nsub, ncall, cps]
-            s.g1 = GroupedSweep(t1, "f32")
+            s.t1 = t1.reshape(ncall, nsub, cps).transpose(1, 0, 2)  # [nsub, ncall, cps]
+            s.g1 = GroupedSweep(s.t1, "u16" if s.u16 else "f32")
             s.sub = torch.empty((ncall * nsub, s.n_ds), dtype=torch.float32, device=self.device)
             # stage 2: [ncall groups][per-call DMs][nsub subbands at their centres]
             _, _, ctr = _delays.subband_layout(self.freqs, nsub)
@@ -363,7 +374,16 @@ class DDplanExecutor(object):
             raw8 = None
         results = []
         for s in self.steps:
-            if s.ds > 1:
+            # the exact 16-bit path needs the raw 8-bit rows and integer pads
+            use16 = s.u16 and raw8 is not None and _is_int_pad16(padval)
+            if s.ds > 1 and use16:
+                x = s.x16
+                if s.n_ds:
+                    call("pdd_downsample_u8_u16", ptr(raw8), self.C, self.N, raw8.stride(0),
+                         s.ds, ptr(x), s.n_ds, stream_ptr())
+            elif s.ds > 1:
+                if s.x is None:
+                    s.x = torch.empty((self.C, s.n_ds), dtype=torch.float32, device=self.device)
                 x = s.x
                 if s.n_ds and raw8 is not None:
                     call("pdd_downsample_u8", ptr(raw8), self.C, self.N, raw8.stride(0), s.ds,
@@ -375,19 +395,29 @@ class DDplanExecutor(object):
                 x = src
             if not s.two_stage:
                 sw = s.sw
-                if sw.dtype == "u8":
-                    if raw8 is not None and _is_int_pad(padval):
-                        x = raw8
-                    else:  # pads that are not 8-bit integers need the float image
-                        if getattr(s, "sw_f32", None) is None:
-                            s.sw_f32 = DMSweep(s.step.DMs, self.freqs, s.dt, cur_dm=self.cur_dm,
-                                               dtype="f32")
-                        sw = s.sw_f32
+                if sw.dtype == "u8" and raw8 is not None and _is_int_pad(padval):
+                    x = raw8
+                elif sw.dtype != "f32" and not (sw.dtype == "u16" and use16):
+                    # pads that are not small integers (or no raw rows): float image
+                    if getattr(s, "sw_f32", None) is None:
+                        s.sw_f32 = DMSweep(s.step.DMs, self.freqs, s.dt, cur_dm=self.cur_dm,
+                                           dtype="f32")
+                    sw = s.sw_f32
                 sw(x, padval=padval, trim=True, out=s.plane)
                 results.append((s.step, s.step.DMs, s.plane[:, :s.n_out]))
                 continue
-            mode, pv = _pad_args(x, padval)
-            s.g1(x, s.n_ds, s.sub, row_g=1, row_d=s.nsub, pad_mode=mode, padvals=pv)
+            g1 = s.g1
+            if s.u16 and not use16:
+                if getattr(s, "g1_f32", None) is None:
+                    s.g1_f32 = GroupedSweep(s.t1, "f32")
+                g1 = s.g1_f32
+            if use16:
+                pv = torch.full((x.shape[0],), float(padval), dtype=torch.float32,
+                                device=x.device) if not isinstance(padval, str) else None
+                mode = _lib.PAD_ROTATE if isinstance(padval, str) else _lib.PAD_VALUE
+            else:
+                mode, pv = _pad_args(x, padval)
+            g1(x, s.n_ds, s.sub, row_g=1, row_d=s.nsub, pad_mode=mode, padvals=pv)
             if s.n_out:
                 # stage 2 pads: those of each pass's subbanded Spectra
                 # (dedisperse(dm, padval) on the subbanded data)
@@ -398,7 +428,7 @@ class DDplanExecutor(object):
 
     def close(self):
         for s in self.steps:
-            for name in ("sw", "sw_f32", "g1", "g2"):
+            for name in ("sw", "sw_f32", "g1", "g1_f32", "g2"):
                 obj = getattr(s, name, None)
                 if obj is not None:
                     obj.close()

@@ -5,7 +5,7 @@ semantics) and the golden two-stage plane."""
 import numpy as np
 import pytest
 
-from conftest import band, u8_data
+from conftest import band, rel_err, u8_data
 from oracle import spectra_oracle as orc
 
 pytestmark = pytest.mark.gpu
@@ -97,3 +97,33 @@ def test_downsample_u8_equals_f32(gpu, factor, N):
     want, _ = orc.downsample(x.astype(np.float64), DT, factor)
     np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
     np.testing.assert_array_equal(a.cpu().numpy().astype(np.float64), want)
+
+
+@pytest.mark.parametrize("padval", [0, 7, 3.5, "mean"])
+def test_executor_u16_steps_and_pads(gpu, padval):
+    """DDplanExecutor on 8-bit rows: downsample <= 4 steps run on the exact
+    16-bit path (pdd_downsample_u8_u16 + u16 grouped sweep) for integer pads
+    and fall back to the float32 image otherwise; ds 8 steps are float32.
+    Every plane equals the per-pass executor (Spectra.subband + dedisperse),
+    bit for bit for integer pads, 1e-5 for fractional ones."""
+    from pypulsar_amd.formats.spectra import Spectra
+    from pypulsar_amd.sweep import DDplanExecutor, execute_plan
+    from pypulsar_amd.utils.ddplan import Observation
+    C, N = 256, 1 << 15
+    freqs = band(C)
+    x = u8_data(C, N, 23)
+    plan = Observation(DT, 1400.0, 300.0, C).gen_ddplan(0.0, 400.0, 16, 0.5)
+    assert [st.downsamp for st in plan.DDsteps] == [4, 8]
+    s = Spectra(freqs, DT, x)
+    ex = DDplanExecutor(plan, freqs, DT, N, raw8=True)
+    assert [st.u16 for st in ex.steps] == [True, False]
+    fast = ex(s, padval=padval)
+    slow = execute_plan(s, plan, padval=padval, trim=True)
+    for (st, dms, plane), (st2, outs) in zip(fast, slow):
+        got = plane.cpu().numpy()
+        ref = np.concatenate([p.cpu().numpy()[:, :got.shape[1]] for _, p in outs])
+        if isinstance(padval, str) or not float(padval).is_integer():
+            assert rel_err(got, ref) <= 1e-5
+        else:
+            np.testing.assert_array_equal(got, ref)
+    ex.close()
