@@ -639,9 +639,9 @@ __device__ __forceinline__ uint32_t add3_u32(uint32_t a, uint32_t b, uint32_t c)
 template <int G, int DPW, int NCW, int NLW, int CC, int NBUF, bool U16 = false>
 __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const float4* __restrict__ R0, int64_t nR, int C, int lo, const int* __restrict__ mt,
-    float* __restrict__ out, int64_t ld_out, int D, int64_t Qs, int64_t t_base, int64_t n_out,
-    int stride, int n_tblk, int n_dblk, int dbg, int64_t row_g, int64_t row_d, int flush_n,
-    float out_bias) {
+    const int* __restrict__ cht, int maxch, float* __restrict__ out, int64_t ld_out, int D,
+    int64_t Qs, int64_t t_base, int64_t n_out, int buf_e, int n_tblk, int n_dblk, int dbg,
+    int64_t row_g, int64_t row_d, int flush_n, float out_bias) {
   // Grouped sweeps: C is the channel count of ONE group; blockIdx.x / (tiles
   // per group) is the group, whose channels are R rows [grp*C, grp*C + C),
   // whose tables are mt[grp][...], and whose trial d lands in plane row
@@ -652,18 +652,16 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   constexpr int SLOT = il_slot(CC, DB);
   constexpr int MA = il_ma(NBUF), MR = il_mr(NBUF);
   constexpr int S = U16 ? 8 : 4;  // samples per 16-byte element (quarters / eighths)
-  static_assert(DPW == 4 && G == (U16 ? 2 : 4) && DPW * CC <= 64,
+  static_assert(DPW == 4 && G == (U16 ? 2 : 4) && DPW * CC <= 64 && CC % 2 == 0,
                 "4 trials per wave, 4 (f32) or 2 (u16) groups; one lane per (channel, trial)");
   static_assert(NBUF >= 2 && MA >= 2 * NBUF - 2 && MR > MA, "ring geometry");
   extern __shared__ __attribute__((aligned(16))) float smf[];
   uint4* img = reinterpret_cast<uint4*>(smf);
-  const int buf_e = CC * stride;
   int* metar = reinterpret_cast<int*>(img + NBUF * buf_e);  // [MR][SLOT]
 
   const int per_grp = n_tblk * n_dblk;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int nchunk = (C + CC - 1) / CC;
   const bool stamps = (dbg & 4) != 0;  // dbg bit 2: per-wave cycle stamps into `out`
 
   // One tile per workgroup.  (A persistent grid -- 256 workgroups walking
@@ -677,6 +675,8 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   const float4* R = R0 + (int64_t)grp * C * nR;                               \
   const int64_t t0 = (int64_t)tblk * Tq;                                      \
   const int* mt_b = mt + ((int64_t)grp * n_dblk + dblk) * C * ROW;            \
+  const int* cht_t = cht + ((int64_t)grp * n_dblk + dblk) * (maxch + 1);       \
+  const int nchunk = cht_t[0];                                                \
   (void)R; (void)t0; (void)mt_b;
   const int tile = blockIdx.x;
   IL_TILE_SETUP
@@ -688,14 +688,21 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const int lw = w - NCW;
     const uint32_t img_lds = lds_addr_of(img);
     int* ring = metar;  // the shared ring (loader 0 fills it)
+    // chunk k = channels c0 .. c0 + ncc - 1 (cht: c0 | ncc << 20), packed
+    // into its buffer at the per-channel offsets of the metadata rows
+    // (loader 0 reads chunk k + MA's table entry one iteration ahead: a
+    // scalar load's latency is not on the loaders' per-chunk path)
+    int e_next = (lw == 0 && MA < nchunk) ? cht_t[1 + MA] : 0;
     auto issue_meta = [&](int k) -> int {
       if (lw != 0 || k >= nchunk) return 0;
-      const int n_int = min(CC, C - k * CC) * ROW;
+      const int e = k < MA ? cht_t[1 + k] : e_next;
+      if (k >= MA && k + 1 < nchunk) e_next = cht_t[2 + k];
+      const int n_int = (e >> 20) * ROW;
       int n = 0;
 #pragma unroll
       for (int m = 0; m < SLOT / 64; ++m) {
         if (m * 64 >= n_int) break;
-        dma_ints(ring + (k % MR) * SLOT + m * 64, mt_b + (int64_t)k * CC * ROW + m * 64,
+        dma_ints(ring + (k % MR) * SLOT + m * 64, mt_b + (int64_t)(e & 0xfffff) * ROW + m * 64,
                  n_int - m * 64, lane);
         ++n;
       }
@@ -705,15 +712,17 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       if (dbg & 1) return 0;
       const int b = k % NBUF;
       const int* ms = ring + (k % MR) * SLOT;
-      const int ncc = min(CC, C - k * CC);
+      const int ncc = __builtin_amdgcn_readfirstlane(ms[DB + 3]) >> 20;
       int n = 0;
 #pragma unroll
       for (int i = 0; i < CC; ++i) {
         if (i >= ncc) break;
         const int bm = __builtin_amdgcn_readfirstlane(ms[i * ROW + DB]);
         const int ne = Tq + __builtin_amdgcn_readfirstlane(ms[i * ROW + DB + 1]);
-        n += stage_il_dma(img_lds + (uint32_t)((b * CC + i) * stride * 16),
-                          R + (int64_t)(k * CC + i) * nR + (t0 + bm - lo), ne, lw, NLW, lane);
+        const int off = __builtin_amdgcn_readfirstlane(ms[i * ROW + DB + 2]);
+        const int c = __builtin_amdgcn_readfirstlane(ms[i * ROW + DB + 3]) & 0xfffff;
+        n += stage_il_dma(img_lds + (uint32_t)((b * buf_e + off) * 16),
+                          R + (int64_t)c * nR + (t0 + bm - lo), ne, lw, NLW, lane);
       }
       return n;
     };
@@ -816,19 +825,20 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     asm volatile("" ::: "memory");
     if (stamps) { tB = __builtin_amdgcn_s_memtime(); ts_poll += tB - tA; }
     const int slot = k % MR;
-    const int ncc = min(CC, C - k * CC);
     // ONE ds_read_b32 brings the wave's DPW shifts of all CC channels of the
     // chunk (lane DPW*i + j = trial j at channel i, as LDS byte offsets: the
     // plan stores them pre-scaled by 16), each broadcast by v_readlane when
     // its reads issue.  (A ds_read_b128 of 4 shifts per channel costs 4 LDS
     // cycles per channel; this costs 2 per chunk plus one VALU per shift:
     // configs[3] u8 288 -> 280 ms, configs[1] u8 32.7 -> 27.3 ms.)
+    // (the shifts include the channel's offset in the packed buffer; row 0's
+    // last field is the chunk's channel count)
+    typedef __attribute__((address_space(3))) int lds_int_t;
     const int ml = min(lane / DPW, CC - 1) * ROW + lane % DPW;
-    const int vmeta = *(const __attribute__((address_space(3))) int*)(uintptr_t)(
-        meta_base + (uint32_t)((slot * SLOT + ml) * 4));
-    auto chan_base = [&](int i) -> uint32_t {
-      return lane_byte + (uint32_t)((b * CC + i) * stride * 16);
-    };
+    const int vmeta = *(const lds_int_t*)(uintptr_t)(meta_base + (uint32_t)((slot * SLOT + ml) * 4));
+    const int ncc = __builtin_amdgcn_readfirstlane(*(const lds_int_t*)(uintptr_t)(
+        lds_addr_of(metar) + (uint32_t)((slot * SLOT + DB + 3) * 4))) >> 20;
+    auto chan_base = [&](int) -> uint32_t { return lane_byte + (uint32_t)(b * buf_e * 16); };
     if (!(dbg & 2)) {
       if constexpr (U16) {
         // one channel: two trials at a time (a full scheduling barrier
@@ -858,58 +868,42 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
           }
         };
         // flush before a chunk could carry a u16 lane past 65535
-        if (since_flush + CC > flush_n) {
+        if (since_flush + ncc > flush_n) {
           since_flush = 0;
           flush16();
         }
-        since_flush += CC;
-        // channel pairs pay on wide chunks; narrower ones (wide-span grids)
-        // measured faster one channel at a time
-        constexpr bool PAIRS = CC >= 8;
-        if (PAIRS && ncc == CC) {
-          // full chunk: channels in pairs (acc + x_c + x_c+1: one v_add3_u32
-          // per two samples), software-pipelined over the (pair, trial)
-          // steps: the reads of step s + PD issue before the adds of step s
-          constexpr int NS = (CC / 2) * DPW;
-          constexpr int PD = 1;  // steps in flight (deeper needs registers we lack)
-          u32x4_t v0[PD][G], v1[PD][G];
-          auto issue = [&](int st) {
-            const int i = 2 * (st / DPW), j = st % DPW;
+        since_flush += ncc;
+        // channel pairs (acc + x_c + x_c+1: one v_add3_u32 per two samples)
+        // while two channels remain, then the odd one
+        u32x4_t v0[G], v1[G];
+        auto pair = [&](int i) {
+          const uint32_t cb = chan_base(i);
+#pragma unroll
+          for (int j = 0; j < DPW; ++j) {
             const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane(vmeta, DPW * i + j);
             const uint32_t s1 = (uint32_t)__builtin_amdgcn_readlane(vmeta, DPW * (i + 1) + j);
-            const uint32_t cb0 = chan_base(i), cb1 = chan_base(i + 1);
 #pragma unroll
             for (int g2 = 0; g2 < G; ++g2) {
-              v0[st % PD][g2] = *(const lds_u32x4_t*)(uintptr_t)(cb0 + s0 + g2 * 1024);
-              v1[st % PD][g2] = *(const lds_u32x4_t*)(uintptr_t)(cb1 + s1 + g2 * 1024);
+              v0[g2] = *(const lds_u32x4_t*)(uintptr_t)(cb + s0 + g2 * 1024);
+              v1[g2] = *(const lds_u32x4_t*)(uintptr_t)(cb + s1 + g2 * 1024);
             }
-          };
-          auto consume = [&](int st) {
-            const int j = st % DPW;
 #pragma unroll
             for (int g2 = 0; g2 < G; ++g2) {
-              const u32x4_t x0 = v0[st % PD][g2], x1 = v1[st % PD][g2];
-              a16[j][g2][0] = add3_u32(a16[j][g2][0], x0.x, x1.x);
-              a16[j][g2][1] = add3_u32(a16[j][g2][1], x0.y, x1.y);
-              a16[j][g2][2] = add3_u32(a16[j][g2][2], x0.z, x1.z);
-              a16[j][g2][3] = add3_u32(a16[j][g2][3], x0.w, x1.w);
+              a16[j][g2][0] = add3_u32(a16[j][g2][0], v0[g2].x, v1[g2].x);
+              a16[j][g2][1] = add3_u32(a16[j][g2][1], v0[g2].y, v1[g2].y);
+              a16[j][g2][2] = add3_u32(a16[j][g2][2], v0[g2].z, v1[g2].z);
+              a16[j][g2][3] = add3_u32(a16[j][g2][3], v0[g2].w, v1[g2].w);
             }
-          };
-#pragma unroll
-          for (int st = 0; st < PD - 1; ++st)
-            if (st < NS) issue(st);
-#pragma unroll
-          for (int st = 0; st < NS; ++st) {
-            if (st + PD - 1 < NS) issue(st + PD - 1);
-            consume(st);
             __builtin_amdgcn_sched_barrier(0);
           }
-          if constexpr (CC & 1) one16(CC - 1);
-        } else {
+        };
 #pragma unroll
-          for (int i = 0; i < CC; ++i) {
-            if (i >= ncc) break;
-            one16(i);
+        for (int i = 0; i < CC; i += 2) {
+          if (i + 1 < ncc) {
+            pair(i);
+          } else {
+            if (i < ncc) one16(i);
+            break;
           }
         }
       } else {
@@ -1328,29 +1322,20 @@ struct Variant {
 // Every entry is reached by a named test (tests/test_gpu_parity.py
 // test_sweep_variant_ladder).
 static const Variant kF32Variants[] = {
-    {0, false, 4, 4, 4, 14, 8, 3, 2},  // DB 56, 8-channel chunks (fewest barriers)
-    {0, false, 4, 4, 4, 14, 4, 4, 2},  //   4-channel chunks
-    {0, false, 4, 4, 4, 14, 4, 3, 2},  //   4-channel chunks, 3 buffers
-    {0, false, 4, 4, 4, 14, 3, 3, 2},  //   3-channel chunks
-    {0, false, 4, 4, 4, 14, 2, 4, 2},  //   2-channel chunks (configs[1]: wide windows)
-    {0, false, 4, 4, 4, 8, 1, 6, 2},   // DB 32
-    {0, false, 4, 4, 4, 4, 1, 3, 2},   // DB 16, 2 workgroups / CU
+    {0, false, 4, 4, 4, 14, 8, 2, 2},  // DB 56, 2 packed buffers of <= 8 channels (configs[1]:
+                                       //   37.9 ms against 39.4 with 3 buffers)
+    {0, false, 4, 4, 4, 8, 8, 2, 2},   // DB 32
     {1, false, 4, 4, 1, 8, 1, 2, 0},   // generic, DB 8
     {1, false, 4, 1, 1, 1, 1, 2, 0}};  // generic, DB 1 (any span that fits 160 KB)
 // 8-bit input: u16 eighths (12 compute + 4 loader waves: with half the
-// compute per staged byte the extra loaders pay off) in chunks as wide as the
-// LDS allows (measured, BASELINE configs[3]: 2 / 3 / 4 / 8 channels per chunk
-// = 376 / 333 / 315 / 298 ms per launch), then the float32-image tilings,
-// then the generic u16 kernel.
+// compute per staged byte the extra loaders pay off), then the float32-image
+// tilings, then the generic u16 kernel.
 static const Variant kU8Variants[] = {
-    {0, false, 8, 2, 4, 12, 8, 3, 4},  // u16 eighths, DB 48, 8-channel chunks
-    {0, false, 8, 2, 4, 12, 4, 4, 4},  //   4-channel chunks
-    {0, false, 8, 2, 4, 12, 4, 3, 4},  //   4-channel chunks, 3 buffers
-    {0, false, 8, 2, 4, 12, 3, 3, 4},  //   3-channel chunks (configs[1])
-    {0, false, 4, 4, 4, 8, 1, 6, 2},   // f32 image of u8 data, DB 32
-    {0, false, 4, 4, 4, 4, 1, 3, 2},   // DB 16
-    {1, true, 8, 2, 1, 8, 1, 2, 0},    // generic u16, DB 8
-    {1, true, 8, 1, 1, 1, 1, 2, 0}};   // generic u16, DB 1
+    {0, false, 8, 2, 4, 12, 16, 3, 4},  // u16 eighths, DB 48, 3 packed buffers of <= 16 channels
+    {0, false, 8, 2, 4, 12, 16, 2, 4},  //   2 buffers (wider windows)
+    {0, false, 4, 4, 4, 8, 8, 2, 2},    // f32 image of u8 data, DB 32
+    {1, true, 8, 2, 1, 8, 1, 2, 0},     // generic u16, DB 8
+    {1, true, 8, 1, 1, 1, 1, 2, 0}};    // generic u16, DB 1
 
 #ifdef PDD_SWEEP_DEV
 // experimental 8-bit MFMA tilings, tried first when PDD_SWEEP_MX=1
@@ -1366,27 +1351,20 @@ static int64_t lds_budget(const Variant& v) {
 }
 static constexpr int kLdsMax = 160 * 1024;
 
-typedef void (*sweep_il_fn)(const float4*, int64_t, int, int, const int*, float*, int64_t, int,
-                            int64_t, int64_t, int64_t, int, int, int, int, int64_t, int64_t, int,
-                            float);
+typedef void (*sweep_il_fn)(const float4*, int64_t, int, int, const int*, const int*, int, float*,
+                            int64_t, int, int64_t, int64_t, int64_t, int, int, int, int, int64_t,
+                            int64_t, int, float);
 static sweep_il_fn il_kernel_for(const Variant& v) {
 #define IL(NCW_, NLW_, CC_, NB_)                                                              \
   if (v.S == 4 && v.NW == NCW_ && v.NLW == NLW_ && v.CC == CC_ && v.NBUF == NB_ && v.G == 4 && \
       v.DPW == 4)                                                                               \
     return k_sweep_il<4, 4, NCW_, NLW_, CC_, NB_>;
   if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.DPW == 4) {
-    if (v.CC == 8 && v.NBUF == 3) return k_sweep_il<2, 4, 12, 4, 8, 3, true>;
-    if (v.CC == 4 && v.NBUF == 4) return k_sweep_il<2, 4, 12, 4, 4, 4, true>;
-    if (v.CC == 4 && v.NBUF == 3) return k_sweep_il<2, 4, 12, 4, 4, 3, true>;
-    if (v.CC == 3 && v.NBUF == 3) return k_sweep_il<2, 4, 12, 4, 3, 3, true>;
+    if (v.CC == 16 && v.NBUF == 3) return k_sweep_il<2, 4, 12, 4, 16, 3, true>;
+    if (v.CC == 16 && v.NBUF == 2) return k_sweep_il<2, 4, 12, 4, 16, 2, true>;
   }
-  IL(14, 2, 8, 3)
-  IL(14, 2, 4, 4)
-  IL(14, 2, 4, 3)
-  IL(14, 2, 3, 3)
-  IL(14, 2, 2, 4)
-  IL(8, 2, 1, 6)
-  IL(4, 2, 1, 3)
+  IL(14, 2, 8, 2)
+  IL(8, 2, 8, 2)
 #undef IL
   return nullptr;
 }
@@ -1452,7 +1430,8 @@ struct pdd_sweep_plan {
   int64_t D, C, Dpad, n_dblk;
   int max_span, stride, cc, lds_bytes;
   int* d_tab = nullptr;    // [C][Dpad] shifts relative to the block minimum
-  int* d_bmin = nullptr;   // [n_dblk][C]
+  int* d_bmin = nullptr;   // [n_dblk][C]; interleaved kernel: chunk tables
+  int maxch = 0;           // interleaved kernel: most chunks of a trial block
   int* d_bspan = nullptr;  // [n_dblk][C]
   int max_bin = 0, min_bin = 0;
   int vi = 0;              // index of the chosen tiling in its candidate list
@@ -1700,8 +1679,8 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
     if (p->timing && !bracket) pm->dropped++;
     if (bracket) (void)hipEventRecord(p->ev[2 * p->timed], st);
     hipLaunchKernelGGL(il_kernel_for(p->v), dim3((unsigned)blocks), dim3(p->v.threads()),
-                       p->lds_bytes, st, R, nR, (int)p->C, (int)lo, p->d_tab, out, ld_out,
-                       (int)p->D, Qs, t_base, t_base + cnt, p->stride, (int)n_tblk,
+                       p->lds_bytes, st, R, nR, (int)p->C, (int)lo, p->d_tab, p->d_bmin, p->maxch,
+                       out, ld_out, (int)p->D, Qs, t_base, t_base + cnt, p->stride, (int)n_tblk,
                        (int)p->n_dblk, dbg, row_g, row_d, flush_n, out_bias);
     if (hipGetLastError() != hipSuccess) rc = -3;
     if (bracket) {
@@ -1749,9 +1728,6 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
     const Variant v = cands[vi];
     const bool il = v.kind == 0;
     if (n_grp > 1 && !il) continue;  // only the interleaved kernel sweeps groups
-    // the global-flush (DB 96) tilings flush every 256 channels (8-bit data
-    // only) and sweep whole chunks (C % CC == 0)
-    if (v.DPW == 8 && (dtype == PDD_U16 || C % v.CC != 0)) continue;
     if (dtype == PDD_U16 && !il) {     // the generic kernel reads 8-bit or float32 rows
       set_error("pdd_sweep_plan_create: DM grid too sparse for a 16-bit-input tile");
       return -1;
@@ -1760,8 +1736,19 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
     const int64_t n_dblk = cdiv(D, DB);
     const int64_t Dpad = n_dblk * DB;
     std::vector<int> mt_all;  // interleaved path: mt of every group, concatenated
+    std::vector<std::vector<int>> chunks;  // interleaved path: per (group, block) chunk list
     int max_span = 0, mx = INT32_MIN, mn = INT32_MAX;
     std::vector<int> tab, bmin, bspan;
+    const bool last = (vi == ncand - 1);
+    // interleaved kernel: NBUF chunk buffers of buf_e 16-B elements each
+    // (what the LDS holds beside the metadata ring); a chunk packs up to CC
+    // channel windows of 64-element DMA granules, Tq + span each
+    int64_t buf_e = 0;
+    bool fits = true;
+    if (il) {
+      const int64_t room = (last ? kLdsMax : lds_budget(v)) - il_meta_bytes(v.NBUF, v.CC, v.DB());
+      buf_e = std::max<int64_t>(0, room / (v.NBUF * 16) / 64 * 64);
+    }
     for (int64_t grp = 0; grp < n_grp; ++grp) {
     const int32_t* htab = host_table + grp * D * C;
     tab.assign((size_t)(C * Dpad), 0);
@@ -1791,29 +1778,59 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
     for (int64_t c = 0; c < C; ++c)
       for (int64_t d = 0; d < Dpad; ++d) tab[(size_t)(c * Dpad + d)] -= bmin[(size_t)((d / DB) * C + c)];
     if (il) {
-      // mt[grp][dblk][c][DB + 4] = shifts rel. to bmin, then {bmin, span, 0, 0}
+      // mt[grp][dblk][c][DB + 4] = the DB shifts as LDS byte offsets in the
+      // chunk buffer (16 x (shift - bmin + channel offset)), then {bmin, span,
+      // channel offset (elements), c | channels in the chunk << 20}; chunks filled
+      // greedily, channel order, up to CC channels or buf_e elements
       const int64_t ROWN = DB + 4;
-      const size_t off = mt_all.size();
-      mt_all.resize(off + (size_t)(n_dblk * C * ROWN), 0);
-      for (int64_t b = 0; b < n_dblk; ++b)
+      const int64_t Tq = 64 * v.G;
+      const size_t moff = mt_all.size();
+      mt_all.resize(moff + (size_t)(n_dblk * C * ROWN), 0);
+      for (int64_t b = 0; b < n_dblk && fits; ++b) {
+        std::vector<int> list;
+        int64_t c0 = 0, used = 0, ncc = 0;
+        auto close = [&]() {
+          for (int64_t c = c0; c < c0 + ncc; ++c)
+            mt_all[moff + (size_t)((b * C + c) * ROWN + DB + 3)] = (int)(c | (ncc << 20));
+          list.push_back((int)(c0 | (ncc << 20)));
+        };
         for (int64_t c = 0; c < C; ++c) {
-          const size_t base = off + (size_t)((b * C + c) * ROWN);
-          // shifts as LDS byte offsets of the 16-B image elements
-          for (int64_t d = 0; d < DB; ++d) mt_all[base + d] = 16 * tab[(size_t)(c * Dpad + b * DB + d)];
+          const int64_t win = (Tq + bspan[(size_t)(b * C + c)] + 63) / 64 * 64;
+          if (win > buf_e) { fits = false; break; }
+          if (ncc == v.CC || used + win > buf_e) {
+            close();
+            c0 = c;
+            used = 0;
+            ncc = 0;
+          }
+          const size_t base = moff + (size_t)((b * C + c) * ROWN);
+          for (int64_t d = 0; d < DB; ++d)
+            mt_all[base + d] = (int)(16 * (tab[(size_t)(c * Dpad + b * DB + d)] + used));
           mt_all[base + DB] = bmin[(size_t)(b * C + c)];
           mt_all[base + DB + 1] = bspan[(size_t)(b * C + c)];
+          mt_all[base + DB + 2] = (int)used;
+          used += win;
+          ++ncc;
         }
+        if (fits) close();
+        chunks.push_back(std::move(list));
+      }
     }
     }  // groups
-    // stride rounded to 16 elements: an LDS-DMA wave-instruction writes 16
-    // whole elements; NBUF chunk buffers of CC channels
-    const int64_t stride = v.stride_for(max_span);
-    const int64_t per_chan = v.NBUF * v.chan_bytes(stride);
-    const bool last = (vi == ncand - 1);
-    // linear kernel: metadata rings (NBUF x 64 ints x 2) after the buffers
-    const int64_t need = per_chan * v.CC + (il ? il_meta_bytes(v.NBUF, v.CC, v.DB()) : 0);
+    // generic kernel: stride rounded to 16 elements, NBUF chunk buffers of
+    // CC channels; interleaved kernel: NBUF packed buffers + the metadata ring
+    const int64_t stride = il ? buf_e : v.stride_for(max_span);
+    const int64_t need = il ? v.NBUF * buf_e * 16 + il_meta_bytes(v.NBUF, v.CC, v.DB())
+                            : v.NBUF * v.chan_bytes(stride) * v.CC;
     if (il && (int64_t)max_span + 64 * v.G > (int64_t)1 << 20) continue;  // windows too wide
-    if (need > lds_budget(v) && !(last && need <= kLdsMax)) {
+    if (il && !fits) {
+      if (last) {
+        set_error("pdd_sweep_plan_create: DM grid too sparse for one LDS tile (span %d bins)", max_span);
+        return -1;
+      }
+      continue;
+    }
+    if (!il && need > lds_budget(v) && !(last && need <= kLdsMax)) {
       if (last) {
         set_error("pdd_sweep_plan_create: DM grid too sparse for one LDS tile (span %d bins)", max_span);
         return -1;
@@ -1834,7 +1851,18 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
     p->vi = vi;
     p->dtype = dtype;
     p->n_grp = n_grp;
-    if (il) tab.swap(mt_all);
+    if (il) {
+      tab.swap(mt_all);
+      // chunk tables [n_grp * n_dblk][1 + maxch]: count, then c0 | ncc << 20
+      size_t maxch = 0;
+      for (const auto& l : chunks) maxch = std::max(maxch, l.size());
+      bmin.assign(chunks.size() * (maxch + 1), 0);
+      for (size_t i = 0; i < chunks.size(); ++i) {
+        bmin[i * (maxch + 1)] = (int)chunks[i].size();
+        for (size_t k = 0; k < chunks[i].size(); ++k) bmin[i * (maxch + 1) + 1 + k] = chunks[i][k];
+      }
+      p->maxch = (int)maxch;
+    }
     p->max_bin = mx;
     p->min_bin = mn;
     hipError_t e = hipMalloc(&p->d_tab, tab.size() * sizeof(int));

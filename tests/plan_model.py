@@ -5,11 +5,9 @@ test_sweep_variant_ladder, which also asserts the library chose the same."""
 import numpy as np
 
 # (kind, u8, S, G, DPW, NW, CC, NBUF, NLW), as in pdd_sweep.hip
-F32 = [(0, 0, 4, 4, 4, 14, 8, 3, 2), (0, 0, 4, 4, 4, 14, 4, 4, 2), (0, 0, 4, 4, 4, 14, 4, 3, 2),
-       (0, 0, 4, 4, 4, 14, 3, 3, 2), (0, 0, 4, 4, 4, 14, 2, 4, 2), (0, 0, 4, 4, 4, 8, 1, 6, 2),
-       (0, 0, 4, 4, 4, 4, 1, 3, 2), (1, 0, 4, 4, 1, 8, 1, 2, 0), (1, 0, 4, 1, 1, 1, 1, 2, 0)]
-U8 = [(0, 0, 8, 2, 4, 12, 8, 3, 4), (0, 0, 8, 2, 4, 12, 4, 4, 4), (0, 0, 8, 2, 4, 12, 4, 3, 4),
-      (0, 0, 8, 2, 4, 12, 3, 3, 4), (0, 0, 4, 4, 4, 8, 1, 6, 2), (0, 0, 4, 4, 4, 4, 1, 3, 2),
+F32 = [(0, 0, 4, 4, 4, 14, 8, 2, 2), (0, 0, 4, 4, 4, 8, 8, 2, 2),
+       (1, 0, 4, 4, 1, 8, 1, 2, 0), (1, 0, 4, 1, 1, 1, 1, 2, 0)]
+U8 = [(0, 0, 8, 2, 4, 12, 16, 3, 4), (0, 0, 8, 2, 4, 12, 16, 2, 4), (0, 0, 4, 4, 4, 8, 8, 2, 2),
       (1, 1, 8, 2, 1, 8, 1, 2, 0), (1, 1, 8, 1, 1, 1, 1, 2, 0)]
 
 
@@ -22,27 +20,32 @@ def _slot(cc, db):
 
 
 def choose(table, dtype):
-    """Index of the candidate the plan takes for an int [D, C] table."""
+    """Index of the candidate the plan takes for an int [D, C] table: the
+    interleaved kernels pack each trial block's channel windows (64-element
+    granules of Tq + span) into NBUF buffers of what the LDS holds beside the
+    metadata ring; the generic kernels need NBUF x CC windows of the widest
+    span."""
     cands = U8 if dtype == "u8" else F32
     D, C = table.shape
     for vi, (kind, u8, S, G, DPW, NW, CC, NBUF, NLW) in enumerate(cands):
         DB = NW * DPW
         nb = -(-D // DB)
         t = table[np.minimum(np.arange(nb * DB), D - 1)].reshape(nb, DB, C)
-        span = int((t.max(axis=1) - t.min(axis=1)).max())
-        if kind == 0:
-            stride = (64 * G + span + 63) // 64 * 64
-            elem = 16
-            need = NBUF * stride * elem * CC + _mr(NBUF) * _slot(CC, DB) * 4
-            budget = 78 * 1024 if (NW + NLW) * 2 <= 16 else 158 * 1024
-            if span + 64 * G > (1 << 20):
-                continue
-        else:
-            stride = (64 * G + span + 15) // 16 * 16
-            elem = 2 * S if u8 else 4 * S
-            need = NBUF * stride * elem * CC
-            budget = 150 * 1024 if NW >= 16 else 76 * 1024
+        spans = t.max(axis=1) - t.min(axis=1)
+        span = int(spans.max())
         last = vi == len(cands) - 1
+        if kind == 0:
+            budget = 78 * 1024 if (NW + NLW) * 2 <= 16 else 158 * 1024
+            room = (160 * 1024 if last else budget) - _mr(NBUF) * _slot(CC, DB) * 4
+            buf_e = max(0, room // (NBUF * 16) // 64 * 64)
+            win = (64 * G + span + 63) // 64 * 64
+            if span + 64 * G > (1 << 20) or win > buf_e:
+                continue
+            return vi
+        stride = (64 * G + span + 15) // 16 * 16
+        elem = 2 * S if u8 else 4 * S
+        need = NBUF * stride * elem * CC
+        budget = 150 * 1024 if NW >= 16 else 76 * 1024
         if need <= budget or (last and need <= 160 * 1024):
             return vi
     return None
