@@ -86,6 +86,53 @@ __global__ __launch_bounds__(256) void k_corner_turn_vec(const InT* __restrict__
   }
 }
 
+// 8-bit raw corner turn [nspec][nchan] -> [nchan][nspec] with 16-byte loads
+// and stores: a tile of 128 spectra x 64 channels goes through LDS as dwords
+// (rows of 17 dwords), each output vector gathers 16 spectra of one channel
+// byte by byte.  Rows and nchan must be 16-B aligned (the launcher checks);
+// the nspec tail is stored bytewise.
+__global__ __launch_bounds__(256) void k_corner_turn_b8v(const uint8_t* __restrict__ in,
+                                                         int64_t nspec, int64_t nchan, int64_t ld_in,
+                                                         uint8_t* __restrict__ out, int64_t ld_out,
+                                                         int64_t tiles_c) {
+  __shared__ uint32_t tile[128][17];
+  const int64_t tt = blockIdx.x / tiles_c, tc = blockIdx.x % tiles_c;
+  const int64_t t0 = tt * 128, c0 = tc * 64;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int r = (threadIdx.x >> 2) + 64 * pass, seg = threadIdx.x & 3;
+    const int64_t t = t0 + r, c = c0 + seg * 16;
+    uint4 q = make_uint4(0u, 0u, 0u, 0u);
+    if (t < nspec && c < nchan) q = *reinterpret_cast<const uint4*>(in + t * ld_in + c);
+    tile[r][seg * 4 + 0] = q.x;
+    tile[r][seg * 4 + 1] = q.y;
+    tile[r][seg * 4 + 2] = q.z;
+    tile[r][seg * 4 + 3] = q.w;
+  }
+  __syncthreads();
+  const auto* tb = reinterpret_cast<const uint8_t*>(&tile[0][0]);
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int cl = (threadIdx.x >> 3) + 32 * pass, ts = threadIdx.x & 7;
+    const int64_t c = c0 + cl, t = t0 + ts * 16;
+    if (c >= nchan || t >= nspec) continue;
+    uint32_t w[4];
+#pragma unroll
+    for (int k4 = 0; k4 < 4; ++k4) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v |= (uint32_t)tb[(ts * 16 + k4 * 4 + k) * 68 + cl] << (8 * k);
+      w[k4] = v;
+    }
+    uint8_t* o = out + c * ld_out + t;
+    if (t + 16 <= nspec) {
+      *reinterpret_cast<uint4*>(o) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+      for (int k = 0; k < (int)(nspec - t); ++k) o[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    }
+  }
+}
+
 template <typename InT>
 __global__ __launch_bounds__(256) void k_convert(const InT* __restrict__ in, int64_t rows,
                                                  int64_t cols, int64_t ld_in,
@@ -992,7 +1039,14 @@ int pdd_corner_turn(const void* in, int in_dtype, int64_t nspec, int64_t nchan, 
     else PDD_REQUIRE(false, "pdd_corner_turn: bad in_dtype %d", in_dtype);
   } else {
     PDD_REQUIRE(out_dtype == in_dtype, "pdd_corner_turn: out dtype must be F32 or the input dtype");
-    if (in_dtype == PDD_U8) CT(uint8_t, uint8_t);
+    if (in_dtype == PDD_U8 && (uintptr_t)in % 16 == 0 && (uintptr_t)out % 16 == 0 &&
+        ld_in % 16 == 0 && nchan % 16 == 0 && ld_out % 16 == 0) {
+      const int64_t tcb = cdiv(nchan, 64);
+      const int64_t bb = cdiv(nspec, 128) * tcb;
+      PDD_REQUIRE(bb < (1ll << 31), "pdd_corner_turn: too large");
+      k_corner_turn_b8v<<<(unsigned)bb, 256, 0, s>>>((const uint8_t*)in, nspec, nchan, ld_in,
+                                                     (uint8_t*)out, ld_out, tcb);
+    } else if (in_dtype == PDD_U8) CT(uint8_t, uint8_t);
     else if (in_dtype == PDD_U16) CT(uint16_t, uint16_t);
     else PDD_REQUIRE(false, "pdd_corner_turn: bad in_dtype %d", in_dtype);
   }

@@ -232,6 +232,24 @@ def test_corner_turn(gpu, dt_):
         np.testing.assert_array_equal(o8.cpu().numpy(), a.T)
 
 
+@pytest.mark.parametrize("nspec,nchan", [(1007, 400), (128, 64), (4096, 4096), (17, 16)])
+def test_corner_turn_b8_vector(gpu, nspec, nchan):
+    """The 16-byte 8-bit raw corner turn (aligned rows): tiles of 128 spectra
+    x 64 channels, partial tiles at both edges, a bytewise nspec tail, and no
+    write past nspec in a padded output row."""
+    import torch
+    from pypulsar_amd import _lib
+    a = np.random.default_rng(5).integers(0, 256, (nspec, nchan), dtype=np.uint8)
+    src = torch.from_numpy(a).cuda()
+    ld_out = (nspec + 15) // 16 * 16 + 16
+    o8 = torch.full((nchan, ld_out), 7, dtype=torch.uint8, device="cuda")
+    _lib.call("pdd_corner_turn", _lib.ptr(src), _lib.U8, nspec, nchan, nchan, _lib.ptr(o8),
+              _lib.U8, ld_out, _lib.stream_ptr())
+    got = o8.cpu().numpy()
+    np.testing.assert_array_equal(got[:, :nspec], a.T)
+    assert (got[:, nspec:] == 7).all()
+
+
 # ------------------------------------------------------------------ sweep
 @pytest.mark.parametrize("dtype", ["f32", "u8"])
 def test_sweep_golden(gpu, golden, dtype):
