@@ -674,7 +674,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   il_tile_of(tile - grp * per_grp, n_tblk, n_dblk, dbg, dblk, tblk);          \
   const float4* R = R0 + (int64_t)grp * C * nR;                               \
   const int64_t t0 = (int64_t)tblk * Tq;                                      \
-  const int* mt_b = mt + ((int64_t)grp * n_dblk + dblk) * C * ROW;            \
+  const int* mt_b = mt + ((int64_t)grp * n_dblk + dblk) * (C + 1) * ROW;      \
   const int* cht_t = cht + ((int64_t)grp * n_dblk + dblk) * (maxch + 1);       \
   const int nchunk = cht_t[0];                                                \
   (void)R; (void)t0; (void)mt_b;
@@ -841,40 +841,15 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     auto chan_base = [&](int) -> uint32_t { return lane_byte + (uint32_t)(b * buf_e * 16); };
     if (!(dbg & 2)) {
       if constexpr (U16) {
-        // one channel: two trials at a time (a full scheduling barrier
-        // between the halves keeps the live read registers within budget)
-        auto one16 = [&](int i) {
-          const uint32_t cb = chan_base(i);
-#pragma unroll
-          for (int jh = 0; jh < DPW; jh += 2) {
-            u32x4_t v[2][G];
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane(vmeta, DPW * i + jh + j);
-#pragma unroll
-              for (int g2 = 0; g2 < G; ++g2)
-                v[j][g2] = *(const lds_u32x4_t*)(uintptr_t)(cb + sj + g2 * 1024);
-            }
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-              for (int g2 = 0; g2 < G; ++g2) {
-                a16[jh + j][g2][0] += v[j][g2].x;
-                a16[jh + j][g2][1] += v[j][g2].y;
-                a16[jh + j][g2][2] += v[j][g2].z;
-                a16[jh + j][g2][3] += v[j][g2].w;
-              }
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        };
         // flush before a chunk could carry a u16 lane past 65535
         if (since_flush + ncc > flush_n) {
           since_flush = 0;
           flush16();
         }
         since_flush += ncc;
-        // channel pairs (acc + x_c + x_c+1: one v_add3_u32 per two samples)
-        // while two channels remain, then the odd one
+        // channel pairs (acc + x_c + x_c+1: one v_add3_u32 per two samples);
+        // u16 chunks always hold an even count (an odd channel count ends in
+        // a pad channel whose window is a row of zeros)
         u32x4_t v0[G], v1[G];
         auto pair = [&](int i) {
           const uint32_t cb = chan_base(i);
@@ -898,14 +873,8 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
           }
         };
 #pragma unroll
-        for (int i = 0; i < CC; i += 2) {
-          if (i + 1 < ncc) {
-            pair(i);
-          } else {
-            if (i < ncc) one16(i);
-            break;
-          }
-        }
+        for (int i = 0; i < CC; i += 2)
+          if (i < ncc) pair(i);
       } else {
 #pragma unroll
         for (int i = 0; i < CC; ++i) {
@@ -1331,8 +1300,9 @@ static const Variant kF32Variants[] = {
 // compute per staged byte the extra loaders pay off), then the float32-image
 // tilings, then the generic u16 kernel.
 static const Variant kU8Variants[] = {
-    {0, false, 8, 2, 4, 12, 16, 3, 4},  // u16 eighths, DB 48, 3 packed buffers of <= 16 channels
-    {0, false, 8, 2, 4, 12, 16, 2, 4},  //   2 buffers (wider windows)
+    {0, false, 8, 2, 4, 12, 8, 3, 4},   // u16 eighths, DB 48, 3 packed buffers of <= 8 channels
+                                        //   (configs[3]: 260 ms against 264 with <= 16)
+    {0, false, 8, 2, 4, 12, 8, 2, 4},   //   2 buffers (wider windows)
     {0, false, 4, 4, 4, 8, 8, 2, 2},    // f32 image of u8 data, DB 32
     {1, true, 8, 2, 1, 8, 1, 2, 0},     // generic u16, DB 8
     {1, true, 8, 1, 1, 1, 1, 2, 0}};    // generic u16, DB 1
@@ -1360,8 +1330,8 @@ static sweep_il_fn il_kernel_for(const Variant& v) {
       v.DPW == 4)                                                                               \
     return k_sweep_il<4, 4, NCW_, NLW_, CC_, NB_>;
   if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.DPW == 4) {
-    if (v.CC == 16 && v.NBUF == 3) return k_sweep_il<2, 4, 12, 4, 16, 3, true>;
-    if (v.CC == 16 && v.NBUF == 2) return k_sweep_il<2, 4, 12, 4, 16, 2, true>;
+    if (v.CC == 8 && v.NBUF == 3) return k_sweep_il<2, 4, 12, 4, 8, 3, true>;
+    if (v.CC == 8 && v.NBUF == 2) return k_sweep_il<2, 4, 12, 4, 8, 2, true>;
   }
   IL(14, 2, 8, 2)
   IL(8, 2, 8, 2)
@@ -1647,13 +1617,15 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
   const int64_t nr_alloc = qs_max + (hi - lo) + 64;
   float4* R = nullptr;
   hipStream_t st = as_stream(stream);
-  PDD_HIP(hipMallocAsync((void**)&R, (size_t)(C * nr_alloc) * sizeof(float4), st));
+  // C rows of the image + one row of zeros (the u16 kernel's pad channel)
+  PDD_HIP(hipMallocAsync((void**)&R, (size_t)((C + 1) * nr_alloc) * sizeof(float4), st));
   const int dbg = debug_flags();
   int rc = 0;
   for (int64_t t_base = 0; t_base < n_out && rc == 0; t_base += seg) {
     const int64_t cnt = std::min(seg, n_out - t_base);
     const int64_t Qs = cdiv(cdiv(cnt, SP), Tq) * Tq;
     const int64_t nR = Qs + (hi - lo) + 64;
+    if (hipMemsetAsync(R + C * nR, 0, (size_t)nR * sizeof(float4), st) != hipSuccess) { rc = -3; break; }
     dim3 g1((unsigned)cdiv(nR, 256 * kIlPer), (unsigned)C);
     if (u16 && p->dtype == PDD_U8)
       hipLaunchKernelGGL(k_interleave_u16<uint8_t>, g1, dim3(256), 0, st, (const uint8_t*)x, lay, N,
@@ -1785,32 +1757,43 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
       const int64_t ROWN = DB + 4;
       const int64_t Tq = 64 * v.G;
       const size_t moff = mt_all.size();
-      mt_all.resize(moff + (size_t)(n_dblk * C * ROWN), 0);
+      mt_all.resize(moff + (size_t)(n_dblk * (C + 1) * ROWN), 0);
+      const bool pairs = v.S == 8;  // the u16 kernel sums channel pairs
       for (int64_t b = 0; b < n_dblk && fits; ++b) {
         std::vector<int> list;
         int64_t c0 = 0, used = 0, ncc = 0;
         auto close = [&]() {
           for (int64_t c = c0; c < c0 + ncc; ++c)
-            mt_all[moff + (size_t)((b * C + c) * ROWN + DB + 3)] = (int)(c | (ncc << 20));
+            mt_all[moff + (size_t)((b * (C + 1) + c) * ROWN + DB + 3)] =
+                (int)((c < C ? c : (n_grp - grp) * C) | (ncc << 20));
           list.push_back((int)(c0 | (ncc << 20)));
         };
-        for (int64_t c = 0; c < C; ++c) {
-          const int64_t win = (Tq + bspan[(size_t)(b * C + c)] + 63) / 64 * 64;
-          if (win > buf_e) { fits = false; break; }
-          if (ncc == v.CC || used + win > buf_e) {
+        // window of channel c (c == C: the pad channel, Tq elements of zeros)
+        auto win_of = [&](int64_t c) -> int64_t {
+          return (Tq + (c < C ? bspan[(size_t)(b * C + c)] : 0) + 63) / 64 * 64;
+        };
+        auto place = [&](int64_t c) {
+          const size_t base = moff + (size_t)((b * (C + 1) + c) * ROWN);
+          for (int64_t d = 0; d < DB; ++d)
+            mt_all[base + d] = (int)(16 * ((c < C ? tab[(size_t)(c * Dpad + b * DB + d)] : 0) + used));
+          mt_all[base + DB] = c < C ? bmin[(size_t)(b * C + c)] : 0;
+          mt_all[base + DB + 1] = c < C ? bspan[(size_t)(b * C + c)] : 0;
+          mt_all[base + DB + 2] = (int)used;
+          used += win_of(c);
+          ++ncc;
+        };
+        const int64_t step = pairs ? 2 : 1;
+        for (int64_t c = 0; c < C; c += step) {
+          const int64_t w = win_of(c) + (pairs ? win_of(c + 1) : 0);
+          if (w > buf_e) { fits = false; break; }
+          if (ncc + step > v.CC || used + w > buf_e) {
             close();
             c0 = c;
             used = 0;
             ncc = 0;
           }
-          const size_t base = moff + (size_t)((b * C + c) * ROWN);
-          for (int64_t d = 0; d < DB; ++d)
-            mt_all[base + d] = (int)(16 * (tab[(size_t)(c * Dpad + b * DB + d)] + used));
-          mt_all[base + DB] = bmin[(size_t)(b * C + c)];
-          mt_all[base + DB + 1] = bspan[(size_t)(b * C + c)];
-          mt_all[base + DB + 2] = (int)used;
-          used += win;
-          ++ncc;
+          place(c);
+          if (pairs) place(c + 1);  // c + 1 == C: the pad channel
         }
         if (fits) close();
         chunks.push_back(std::move(list));

@@ -7,7 +7,7 @@ import numpy as np
 # (kind, u8, S, G, DPW, NW, CC, NBUF, NLW), as in pdd_sweep.hip
 F32 = [(0, 0, 4, 4, 4, 14, 8, 2, 2), (0, 0, 4, 4, 4, 8, 8, 2, 2),
        (1, 0, 4, 4, 1, 8, 1, 2, 0), (1, 0, 4, 1, 1, 1, 1, 2, 0)]
-U8 = [(0, 0, 8, 2, 4, 12, 16, 3, 4), (0, 0, 8, 2, 4, 12, 16, 2, 4), (0, 0, 4, 4, 4, 8, 8, 2, 2),
+U8 = [(0, 0, 8, 2, 4, 12, 8, 3, 4), (0, 0, 8, 2, 4, 12, 8, 2, 4), (0, 0, 4, 4, 4, 8, 8, 2, 2),
       (1, 1, 8, 2, 1, 8, 1, 2, 0), (1, 1, 8, 1, 1, 1, 1, 2, 0)]
 
 
@@ -38,8 +38,12 @@ def choose(table, dtype):
             budget = 78 * 1024 if (NW + NLW) * 2 <= 16 else 158 * 1024
             room = (160 * 1024 if last else budget) - _mr(NBUF) * _slot(CC, DB) * 4
             buf_e = max(0, room // (NBUF * 16) // 64 * 64)
-            win = (64 * G + span + 63) // 64 * 64
-            if span + 64 * G > (1 << 20) or win > buf_e:
+            win = (64 * G + spans + 63) // 64 * 64           # [nb, C]
+            if S == 8:  # u16: channels in pairs (odd C: the last with a pad window)
+                if C % 2:
+                    win = np.concatenate([win, np.full((nb, 1), 64 * G)], axis=1)
+                win = win[:, 0::2] + win[:, 1::2]
+            if span + 64 * G > (1 << 20) or int(win.max()) > buf_e:
                 continue
             return vi
         stride = (64 * G + span + 15) // 16 * 16
