@@ -203,6 +203,37 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
 int pdd_sweep_execute_grouped(const pdd_sweep_plan* plan, const void* x, int64_t N, int64_t ld,
                               int pad_mode, const float* padvals, float* out, int64_t ld_out,
                               int64_t n_out, int64_t row_g, int64_t row_d, void* stream);
+/* Sweep of an 8-bit block downsampled by ds (2..4) on the fly: x8 is
+ * channel-major [C_all][ld] uint8 at the raw rate (n_raw samples); the swept
+ * series is Spectra.downsample(ds) of it (formats/spectra.py:329-351: N =
+ * n_raw / ds co-adds, exact integers <= 1020), so the plan must be PDD_U16.
+ * Grouped and ungrouped plans (ungrouped: row_g 0, row_d 1); pads act on the
+ * downsampled series (integers <= 1023 or PDD_PAD_ROTATE).  Replaces
+ * pdd_downsample_u8_u16 + pdd_sweep_execute(_grouped) of a DDplan step
+ * (utils/DDplan2b.py:102-199 downsamp) without the downsampled copy. */
+int pdd_sweep_execute_ds(const pdd_sweep_plan* plan, const uint8_t* x8, int64_t n_raw, int64_t ld,
+                         int64_t ds, int pad_mode, const float* padvals, float* out,
+                         int64_t ld_out, int64_t n_out, int64_t row_g, int64_t row_d,
+                         void* stream);
+/* Both stages of a subbanded DDplan step in two launches and no subband
+ * plane: stage 1 (plan1: grouped, one group per subband, trials = the passes'
+ * subDMs; PDD_U8 rows at ds 1 or PDD_U16 with x = 8-bit rows co-added by
+ * ds 2..4 on the fly, as pdd_sweep_execute_ds) writes its rows -- trial d of
+ * group g = stage-2 channel d * n_grp1 + g, i.e. the subbands of pass d --
+ * directly as stage 2's float32 quarters image; stage 2 (plan2: PDD_F32,
+ * grouped, one group per pass, delays >= 0) sweeps that image into out (trial
+ * d of group g at row g*row_g + d*row_d, n_out columns).  pad2vals[c]: the
+ * value pad of stage-2 channel c (Spectra.dedisperse padval on the subbanded
+ * data).  Equals pdd_sweep_execute(_grouped/_ds) of stage 1 into a
+ * [n_grp2*C2][N1] subband plane followed by pdd_sweep_execute_grouped of
+ * stage 2 over it (formats/spectra.py:96-138 then :229-260 per pass).
+ * Returns -2, with nothing launched, for a block/grid it cannot chain (a
+ * stage that needs more than one segment, or a stage-2 delay span wider than
+ * an eighth of the block): run the two stages apart then. */
+int pdd_subband_chain(const pdd_sweep_plan* plan1, const void* x, int64_t n_raw, int64_t ld,
+                      int64_t ds, int pad1_mode, const float* pad1vals,
+                      const pdd_sweep_plan* plan2, const float* pad2vals, float* out,
+                      int64_t ld_out, int64_t n_out, int64_t row_g, int64_t row_d, void* stream);
 /* Extents used by the plan (for DESIGN/bench reporting): DM trials, channels,
  * DMs per block, time samples per block, LDS bytes per workgroup. */
 int pdd_sweep_plan_info(const pdd_sweep_plan* plan, int64_t* info /*[8]*/);

@@ -35,6 +35,7 @@ EXPORTS = (
     "pdd_sweep_plan_create_grouped", "pdd_sweep_execute_grouped", "pdd_sp_chunk_stats",
     "pdd_sp_search", "pdd_psrfits_subints", "pdd_downsample_u8", "pdd_sweep_timing_read",
     "pdd_sweep_execute_ex", "pdd_zdm_int_downsample", "pdd_downsample_u8_u16",
+    "pdd_sweep_execute_ds", "pdd_subband_chain",
 )
 
 
@@ -80,6 +81,10 @@ _SIGS = {
     "pdd_sweep_plan_create_grouped": ([_vp, _i64, _i64, _i64, _int, ctypes.POINTER(_vp)], _int),
     "pdd_sweep_execute_grouped": ([_vp, _vp, _i64, _i64, _int, _vp, _vp, _i64, _i64, _i64, _i64,
                                    _vp], _int),
+    "pdd_sweep_execute_ds": ([_vp, _vp, _i64, _i64, _i64, _int, _vp, _vp, _i64, _i64, _i64, _i64,
+                              _vp], _int),
+    "pdd_subband_chain": ([_vp, _vp, _i64, _i64, _i64, _int, _vp, _vp, _vp, _vp, _i64, _i64,
+                           _i64, _i64, _vp], _int),
     "pdd_sweep_kernel_ms": ([_vp, ctypes.POINTER(ctypes.c_float)], _int),
     "pdd_sweep_timing_read": ([_vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(_i64)], _int),
     "pdd_sp_chunk_stats": ([_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp], _int),

@@ -533,6 +533,112 @@ __global__ __launch_bounds__(256) void k_interleave_u16(const InT* __restrict__ 
   }
 }
 
+// The same u16 eighths of an 8-bit block DOWNSAMPLED by F <= 4 on the fly
+// (formats/spectra.py:329-351: sample s = the co-add of raw samples
+// s*F .. s*F + F - 1, <= 1020, exact), so a downsampled DDplan step never
+// writes and re-reads its downsampled copy; pads and rotation act on the
+// downsampled series (N = raw length / F) as for k_interleave_u16.  VEC: the
+// F raw bytes of a sample are one aligned 2- or 4-byte load (summed by
+// v_sad_u8 against zero).
+template <int F, bool VEC>
+__global__ __launch_bounds__(256) void k_interleave_u16_ds(const uint8_t* __restrict__ x, int64_t ld,
+                                                           int64_t N, int64_t base, int64_t Qs,
+                                                           int64_t nR, int pad_mode,
+                                                           const float* __restrict__ padvals,
+                                                           uint4* __restrict__ R) {
+  const int c = blockIdx.y;
+  const int64_t j0 = (int64_t)blockIdx.x * (256 * kIlPer) + threadIdx.x;
+  const uint32_t pv = (pad_mode == PDD_PAD_VALUE) ? (uint32_t)padvals[c] : 0u;
+  const uint8_t* row = x + (int64_t)c * ld;
+  auto coadd = [&](int64_t s) -> uint32_t {
+    const uint8_t* q = row + s * F;
+    if constexpr (VEC && F == 4) {
+      return __builtin_amdgcn_sad_u8(*reinterpret_cast<const uint32_t*>(q), 0u, 0u);
+    } else if constexpr (VEC && F == 2) {
+      return __builtin_amdgcn_sad_u8((uint32_t)*reinterpret_cast<const uint16_t*>(q), 0u, 0u);
+    } else {
+      uint32_t a = 0;
+#pragma unroll
+      for (int k = 0; k < F; ++k) a += q[k];
+      return a;
+    }
+  };
+  uint32_t v[kIlPer][8];
+#pragma unroll
+  for (int i = 0; i < kIlPer; ++i)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t s = base + j0 + i * 256 + k * Qs;
+      if (s >= 0 && s < N) v[i][k] = coadd(s);
+      else if (pad_mode == PDD_PAD_ROTATE) v[i][k] = coadd(wrap_mod(s, N));
+      else v[i][k] = pv;
+    }
+#pragma unroll
+  for (int i = 0; i < kIlPer; ++i) {
+    const int64_t j = j0 + i * 256;
+    if (j < nR)
+      R[(int64_t)c * nR + j] = make_uint4(v[i][0] | (v[i][1] << 16), v[i][2] | (v[i][3] << 16),
+                                          v[i][4] | (v[i][5] << 16), v[i][6] | (v[i][7] << 16));
+  }
+}
+
+// Vector form for 16-B aligned rows (F = 2 or 4): a thread builds J = 16 / F
+// CONSECUTIVE elements from one 16-byte load per eighth (J co-adds), and
+// stores them as J contiguous 16-byte elements (a wave writes 4-8 KiB in one
+// piece); the element run's base must be a multiple of J (base % J == 0,
+// Qs % J == 0).  Runs that touch a pad or the wrap take the per-sample path.
+template <int F>
+__global__ __launch_bounds__(256) void k_interleave_u16_ds_v(const uint8_t* __restrict__ x,
+                                                             int64_t ld, int64_t N, int64_t base,
+                                                             int64_t Qs, int64_t nR, int pad_mode,
+                                                             const float* __restrict__ padvals,
+                                                             uint4* __restrict__ R) {
+  static_assert(F == 2 || F == 4, "16-byte loads of 4 or 8 co-adds");
+  constexpr int J = 16 / F;
+  const int c = blockIdx.y;
+  const int64_t j0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * J;
+  if (j0 >= nR) return;
+  const uint32_t pv = (pad_mode == PDD_PAD_VALUE) ? (uint32_t)padvals[c] : 0u;
+  const uint8_t* row = x + (int64_t)c * ld;
+  uint32_t v[8][J];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t s0 = base + j0 + k * Qs;
+    if (s0 >= 0 && s0 + J <= N) {
+      const uint4 q = *reinterpret_cast<const uint4*>(row + s0 * F);
+      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        if constexpr (F == 4) {
+          v[k][h] = __builtin_amdgcn_sad_u8(w[h], 0u, 0u);
+        } else {
+          v[k][2 * h] = __builtin_amdgcn_sad_u8(w[h] & 0xffffu, 0u, 0u);
+          v[k][2 * h + 1] = __builtin_amdgcn_sad_u8(w[h] >> 16, 0u, 0u);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < J; ++e) {
+        const int64_t s = s0 + e;
+        const int64_t sw = (s >= 0 && s < N) ? s : (pad_mode == PDD_PAD_ROTATE ? wrap_mod(s, N) : -1);
+        uint32_t a = pv;
+        if (sw >= 0) {
+          a = 0;
+#pragma unroll
+          for (int f = 0; f < F; ++f) a += row[sw * F + f];
+        }
+        v[k][e] = a;
+      }
+    }
+  }
+  uint4* dst = R + (int64_t)c * nR + j0;
+#pragma unroll
+  for (int e = 0; e < J; ++e)
+    if (j0 + e < nR)
+      dst[e] = make_uint4(v[0][e] | (v[1][e] << 16), v[2][e] | (v[3][e] << 16),
+                          v[4][e] | (v[5][e] << 16), v[6][e] | (v[7][e] << 16));
+}
+
 // n DMAs of 64 elements (1 KiB) each, q = first, first + step, ...
 __device__ __forceinline__ int stage_il_dma(uint32_t lds_dst, const float4* src, int ne, int first,
                                             int step, int lane) {
@@ -641,7 +747,8 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const float4* __restrict__ R0, int64_t nR, int C, int lo, const int* __restrict__ mt,
     const int* __restrict__ cht, int maxch, float* __restrict__ out, int64_t ld_out, int D,
     int64_t Qs, int64_t t_base, int64_t n_out, int buf_e, int n_tblk, int n_dblk, int dbg,
-    int64_t row_g, int64_t row_d, int flush_n, float out_bias) {
+    int64_t row_g, int64_t row_d, int flush_n, float out_bias, const float* __restrict__ r2_pad,
+    int64_t r2_nR, int64_t r2_ov) {
   // Grouped sweeps: C is the channel count of ONE group; blockIdx.x / (tiles
   // per group) is the group, whose channels are R rows [grp*C, grp*C + C),
   // whose tables are mt[grp][...], and whose trial d lands in plane row
@@ -919,6 +1026,40 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     return;
   }
   const int d0 = dblk * DB + w * DPW;
+  if constexpr (S == 8) {
+    if (r2_pad) {
+      // Output as the NEXT sweep's float32 quarters image (subband chain,
+      // pdd_subband_chain): row r = grp*row_g + d*row_d of R2 ([rows][r2_nR]
+      // float4, quarter length Q2 = 2 Qs, single segment, t_base 0) holds
+      //   R2[r][j] = (X(j), X(j + Q2), X(j + 2 Q2), X(j + 3 Q2)),  j < r2_nR,
+      // X(t) = this sweep's sample t (t < n_out) or the next sweep's pad
+      // r2_pad[r].  A lane's eighths (e + k Qs, k < 8) are elements e (even k)
+      // and e + Qs (odd k), and its even eighths 2, 4, 6 + the pad are element
+      // Q2 + e of the overlap tail (e < r2_ov = r2_nR - Q2 <= Qs).
+      float4* R2 = reinterpret_cast<float4*>(out);
+#pragma unroll
+      for (int j = 0; j < DPW; ++j) {
+        const int d = d0 + j;
+        if (d >= D) continue;
+        const int64_t r = (int64_t)grp * row_g + (int64_t)d * row_d;
+        const float pv = r2_pad[r];
+        float4* rrow = R2 + r * r2_nR;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const int64_t e = t0 + g * 64 + lane;
+          if (e >= Qs) continue;
+          float x8[8];
+#pragma unroll
+          for (int k2 = 0; k2 < 8; ++k2)
+            x8[k2] = (e + k2 * Qs < n_out) ? acc[j][g][k2 >> 1][k2 & 1] + out_bias : pv;
+          rrow[e] = make_float4(x8[0], x8[2], x8[4], x8[6]);
+          rrow[e + Qs] = make_float4(x8[1], x8[3], x8[5], x8[7]);
+          if (e < r2_ov) rrow[2 * Qs + e] = make_float4(x8[2], x8[4], x8[6], pv);
+        }
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < DPW; ++j) {
     const int d = d0 + j;
@@ -1323,7 +1464,7 @@ static constexpr int kLdsMax = 160 * 1024;
 
 typedef void (*sweep_il_fn)(const float4*, int64_t, int, int, const int*, const int*, int, float*,
                             int64_t, int, int64_t, int64_t, int64_t, int, int, int, int, int64_t,
-                            int64_t, int, float);
+                            int64_t, int, float, const float*, int64_t, int64_t);
 static sweep_il_fn il_kernel_for(const Variant& v) {
 #define IL(NCW_, NLW_, CC_, NB_)                                                              \
   if (v.S == 4 && v.NW == NCW_ && v.NLW == NLW_ && v.CC == CC_ && v.NBUF == NB_ && v.G == 4 && \
@@ -1591,10 +1732,36 @@ static int execute_mx(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
 // Interleaved path: the output is produced in time segments whose
 // interleaved copy R fits a scratch budget (stream-ordered allocation, freed
 // after the segment loop); each segment is one k_interleave + one k_sweep_il.
+// IlExtra.ds > 1: x is the 8-bit block at the raw rate (channel-major rows
+// of N * ds samples, lay.ld apart), co-added by ds in the interleave
+// pre-pass.  IlExtra.r2_pad: the output is the next sweep's quarters image
+// (k_sweep_il's R2 epilogue; one segment).  IlExtra.R_pre: the image of this
+// sweep was built by the previous one (quarter length Qs_pre, nR_pre
+// elements per row): no interleave pre-pass, one segment.
+// Output samples one segment of the interleaved path can hold (<= 0: the
+// delay span alone exceeds the scratch budget of R).
+static int64_t il_seg_samples(const pdd_sweep_plan* p) {
+  const int Tq = 64 * p->v.G;
+  const int64_t C = p->C * p->n_grp;
+  const int64_t lo = std::min(0, p->min_bin), hi = std::max(0, p->max_bin);
+  int64_t budget = (int64_t)8 << 30;  // bytes of R per segment
+  if (const char* e = getenv("PDD_SWEEP_SEG_BYTES")) budget = std::max<int64_t>(atoll(e), 1 << 16);
+  const int64_t nr_max = budget / (C * 16);
+  return (nr_max - (hi - lo) - 64) / Tq * Tq * p->v.S;
+}
+
+struct IlExtra {
+  int ds = 1;
+  const float* r2_pad = nullptr;
+  int64_t r2_nR = 0, r2_ov = 0;
+  const float4* R_pre = nullptr;
+  int64_t Qs_pre = 0, nR_pre = 0;
+};
 static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayout lay,
                       int64_t x_off, int pad_mode, const float* padvals, float* out,
                       int64_t ld_out, int64_t n_out, int64_t row_g, int64_t row_d, float out_bias,
-                      void* stream) {
+                      void* stream, const IlExtra& ex = IlExtra()) {
+  const int ds = ex.ds;
   const int Tq = 64 * p->v.G;
   const int SP = p->v.S;  // samples per element: 4 (float32 quarters) or 8 (u16 eighths)
   const bool u16 = (SP == 8);
@@ -1603,10 +1770,7 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
   const int flush_n = p->dtype == PDD_U8 ? 256 : 64;
   const int64_t C = p->C * p->n_grp;  // all channels (groups are contiguous channel ranges)
   const int64_t lo = std::min(0, p->min_bin), hi = std::max(0, p->max_bin);
-  int64_t budget = (int64_t)8 << 30;  // bytes of R per segment
-  if (const char* e = getenv("PDD_SWEEP_SEG_BYTES")) budget = std::max<int64_t>(atoll(e), 1 << 16);
-  const int64_t nr_max = budget / (C * 16);
-  int64_t seg = (nr_max - (hi - lo) - 64) / Tq * Tq * SP;  // output samples per segment
+  int64_t seg = il_seg_samples(p);  // output samples per segment
   PDD_REQUIRE(seg > 0, "pdd_sweep_execute: delay span %lld too wide for the segment budget",
               (long long)(hi - lo));
   // equal segments (whole tiles): every launch does the same work
@@ -1615,19 +1779,53 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
   seg = cdiv(cdiv(n_out, nseg), tile_s) * tile_s;
   const int64_t qs_max = seg / SP;
   const int64_t nr_alloc = qs_max + (hi - lo) + 64;
+  PDD_REQUIRE(!(ex.r2_pad || ex.R_pre) || nseg == 1,
+              "pdd_subband_chain: the stages need one segment each (%lld)", (long long)nseg);
+  if (ex.R_pre)
+    PDD_REQUIRE(lo == 0 && n_out <= SP * ex.Qs_pre && ex.Qs_pre % Tq == 0 &&
+                    ex.nR_pre >= ex.Qs_pre + hi + 64 && !u16,
+                "pdd_subband_chain: stage-2 image does not cover this plan");
   float4* R = nullptr;
   hipStream_t st = as_stream(stream);
   // C rows of the image + one row of zeros (the u16 kernel's pad channel)
-  PDD_HIP(hipMallocAsync((void**)&R, (size_t)((C + 1) * nr_alloc) * sizeof(float4), st));
+  if (!ex.R_pre)
+    PDD_HIP(hipMallocAsync((void**)&R, (size_t)((C + 1) * nr_alloc) * sizeof(float4), st));
   const int dbg = debug_flags();
   int rc = 0;
   for (int64_t t_base = 0; t_base < n_out && rc == 0; t_base += seg) {
     const int64_t cnt = std::min(seg, n_out - t_base);
-    const int64_t Qs = cdiv(cdiv(cnt, SP), Tq) * Tq;
-    const int64_t nR = Qs + (hi - lo) + 64;
-    if (hipMemsetAsync(R + C * nR, 0, (size_t)nR * sizeof(float4), st) != hipSuccess) { rc = -3; break; }
+    const int64_t Qs = ex.R_pre ? ex.Qs_pre : cdiv(cdiv(cnt, SP), Tq) * Tq;
+    const int64_t nR = ex.R_pre ? ex.nR_pre : Qs + (hi - lo) + 64;
+    if (ex.r2_pad && ex.r2_nR != 2 * Qs + ex.r2_ov) { rc = -4; break; }
     dim3 g1((unsigned)cdiv(nR, 256 * kIlPer), (unsigned)C);
-    if (u16 && p->dtype == PDD_U8)
+    if (ex.R_pre) {
+      // image built by the previous sweep
+    } else if (hipMemsetAsync(R + C * nR, 0, (size_t)nR * sizeof(float4), st) != hipSuccess) {
+      rc = -3;
+      break;
+    } else if (ds > 1) {
+      const bool vec = ds != 3 && (uintptr_t)x % ds == 0 && lay.ld % ds == 0;
+      const int64_t b0 = t_base + lo + x_off;
+      const int J = 16 / (int)ds;
+      const bool vec16 = ds != 3 && (uintptr_t)x % 16 == 0 && lay.ld % 16 == 0 && b0 % J == 0 &&
+                         Qs % J == 0;
+      const dim3 gv((unsigned)cdiv(nR, 256 * J), (unsigned)C);
+#define ILDS(F_, V_)                                                                           \
+  hipLaunchKernelGGL((k_interleave_u16_ds<F_, V_>), g1, dim3(256), 0, st, (const uint8_t*)x, \
+                     lay.ld, N, b0, Qs, nR, pad_mode, padvals, (uint4*)R)
+      if (vec16 && ds == 2)
+        hipLaunchKernelGGL(k_interleave_u16_ds_v<2>, gv, dim3(256), 0, st, (const uint8_t*)x,
+                           lay.ld, N, b0, Qs, nR, pad_mode, padvals, (uint4*)R);
+      else if (vec16)
+        hipLaunchKernelGGL(k_interleave_u16_ds_v<4>, gv, dim3(256), 0, st, (const uint8_t*)x,
+                           lay.ld, N, b0, Qs, nR, pad_mode, padvals, (uint4*)R);
+      else if (ds == 2 && vec) ILDS(2, true);
+      else if (ds == 2) ILDS(2, false);
+      else if (ds == 3) ILDS(3, false);
+      else if (vec) ILDS(4, true);
+      else ILDS(4, false);
+#undef ILDS
+    } else if (u16 && p->dtype == PDD_U8)
       hipLaunchKernelGGL(k_interleave_u16<uint8_t>, g1, dim3(256), 0, st, (const uint8_t*)x, lay, N,
                          t_base + lo + x_off, Qs, nR, pad_mode, padvals, (uint4*)R);
     else if (u16)
@@ -1651,16 +1849,18 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
     if (p->timing && !bracket) pm->dropped++;
     if (bracket) (void)hipEventRecord(p->ev[2 * p->timed], st);
     hipLaunchKernelGGL(il_kernel_for(p->v), dim3((unsigned)blocks), dim3(p->v.threads()),
-                       p->lds_bytes, st, R, nR, (int)p->C, (int)lo, p->d_tab, p->d_bmin, p->maxch,
-                       out, ld_out, (int)p->D, Qs, t_base, t_base + cnt, p->stride, (int)n_tblk,
-                       (int)p->n_dblk, dbg, row_g, row_d, flush_n, out_bias);
+                       p->lds_bytes, st, ex.R_pre ? ex.R_pre : R, nR, (int)p->C, (int)lo, p->d_tab,
+                       p->d_bmin, p->maxch, out, ld_out, (int)p->D, Qs, t_base, t_base + cnt,
+                       p->stride, (int)n_tblk, (int)p->n_dblk, dbg, row_g, row_d, flush_n, out_bias,
+                       ex.r2_pad, ex.r2_nR, ex.r2_ov);
     if (hipGetLastError() != hipSuccess) rc = -3;
     if (bracket) {
       (void)hipEventRecord(p->ev[2 * p->timed + 1], st);
       pm->timed++;
     }
   }
-  (void)hipFreeAsync(R, st);
+  if (R) (void)hipFreeAsync(R, st);
+  if (rc == -4) set_error("pdd_subband_chain: stage-2 image geometry mismatch");
   if (rc == -1) set_error("pdd_sweep_execute: grid too large");
   if (rc == -3) set_error("pdd_sweep_execute: kernel launch failed");
   return rc;
@@ -1949,6 +2149,84 @@ int pdd_sweep_execute_grouped(const pdd_sweep_plan* p, const void* x, int64_t N,
   if (n_out == 0) return 0;
   return execute_il(p, x, N, InLayout{ld, 0, 0, 0}, 0, pad_mode, padvals, out, ld_out, n_out, row_g,
                     row_d, 0.f, stream);
+}
+
+int pdd_sweep_execute_ds(const pdd_sweep_plan* p, const uint8_t* x8, int64_t n_raw, int64_t ld,
+                         int64_t ds, int pad_mode, const float* padvals, float* out,
+                         int64_t ld_out, int64_t n_out, int64_t row_g, int64_t row_d,
+                         void* stream) {
+  PDD_REQUIRE(p && x8 && out, "pdd_sweep_execute_ds: null pointer");
+  PDD_REQUIRE(p->v.kind == 0 && p->v.S == 8 && p->dtype == PDD_U16,
+              "pdd_sweep_execute_ds: needs a PDD_U16 plan on the 16-bit interleaved tiling");
+  PDD_REQUIRE(ds >= 2 && ds <= 4, "pdd_sweep_execute_ds: downsample factor %lld not in 2..4",
+              (long long)ds);
+  const int64_t N = n_raw / ds;
+  PDD_REQUIRE(N >= 0 && ld >= n_raw && n_out >= 0 && n_out <= N && ld_out >= n_out && row_g >= 0 &&
+                  row_d >= 0,
+              "pdd_sweep_execute_ds: bad shape");
+  PDD_REQUIRE(pad_mode == PDD_PAD_ROTATE || (pad_mode == PDD_PAD_VALUE && padvals),
+              "pdd_sweep_execute_ds: bad pad mode %d", pad_mode);
+  if (n_out == 0) return 0;
+  IlExtra ex;
+  ex.ds = (int)ds;
+  return execute_il(p, x8, N, InLayout{ld, 0, 0, 0}, 0, pad_mode, padvals, out, ld_out, n_out,
+                    p->n_grp > 1 ? row_g : 0, row_d, 0.f, stream, ex);
+}
+
+int pdd_subband_chain(const pdd_sweep_plan* p1, const void* x, int64_t n_raw, int64_t ld, int64_t ds,
+                      int pad1_mode, const float* pad1vals, const pdd_sweep_plan* p2,
+                      const float* pad2vals, float* out, int64_t ld_out, int64_t n_out,
+                      int64_t row_g, int64_t row_d, void* stream) {
+  PDD_REQUIRE(p1 && p2 && x && out && pad2vals, "pdd_subband_chain: null pointer");
+  PDD_REQUIRE(p1->v.kind == 0 && p1->v.S == 8 &&
+                  ((p1->dtype == PDD_U8 && ds == 1) || (p1->dtype == PDD_U16 && ds >= 2 && ds <= 4)),
+              "pdd_subband_chain: stage 1 needs an 8-bit (ds 1) or 16-bit (ds 2..4) plan on the "
+              "16-bit interleaved tiling");
+  PDD_REQUIRE(p2->v.kind == 0 && p2->v.S == 4 && p2->dtype == PDD_F32 && p2->min_bin >= 0,
+              "pdd_subband_chain: stage 2 needs a float32 interleaved plan with delays >= 0");
+  PDD_REQUIRE(p2->C * p2->n_grp == p1->D * p1->n_grp,
+              "pdd_subband_chain: stage-2 channels (%lld) != stage-1 rows (%lld)",
+              (long long)(p2->C * p2->n_grp), (long long)(p1->D * p1->n_grp));
+  PDD_REQUIRE(pad1_mode == PDD_PAD_ROTATE || (pad1_mode == PDD_PAD_VALUE && pad1vals),
+              "pdd_subband_chain: bad pad mode %d", pad1_mode);
+  const int64_t N1 = n_raw / ds;
+  PDD_REQUIRE(N1 > 0 && ld >= n_raw && n_out >= 0 && n_out <= N1 && ld_out >= n_out &&
+                  row_g >= 0 && row_d >= 0,
+              "pdd_subband_chain: bad shape");
+  if (n_out == 0) return 0;
+  // stage 1 covers N1 samples in one segment of eighth length Qs1; stage 2
+  // reads quarters of length 2 Qs1 (a multiple of its 256-element tile)
+  const int64_t Qs1 = cdiv(cdiv(N1, 8), 64 * p1->v.G) * (64 * p1->v.G);
+  const int64_t ov = std::max(0, p2->max_bin) + 64;
+  if (!(ov <= Qs1 && (2 * Qs1) % (64 * p2->v.G) == 0 && il_seg_samples(p1) >= N1 &&
+        il_seg_samples(p2) >= n_out)) {
+    set_error("pdd_subband_chain: block of %lld samples does not chain (stage-2 span %d, "
+              "one segment per stage needed)", (long long)N1, p2->max_bin);
+    return -2;  // nothing launched: run the stages apart
+  }
+  const int64_t C2 = p2->C * p2->n_grp;
+  const int64_t nR2 = 2 * Qs1 + ov;
+  float4* R2 = nullptr;
+  hipStream_t st = as_stream(stream);
+  PDD_HIP(hipMallocAsync((void**)&R2, (size_t)(C2 * nR2) * sizeof(float4), st));
+  IlExtra e1;
+  e1.ds = (int)ds;
+  e1.r2_pad = pad2vals;
+  e1.r2_nR = nR2;
+  e1.r2_ov = ov;
+  // stage-1 rows (= stage-2 channels): trial d of group g -> row d * n_grp1 + g
+  int rc = execute_il(p1, x, N1, InLayout{ld, 0, 0, 0}, 0, pad1_mode, pad1vals, (float*)R2, 0, N1,
+                      1, p1->n_grp, 0.f, stream, e1);
+  if (rc == 0) {
+    IlExtra e2;
+    e2.R_pre = R2;
+    e2.Qs_pre = 2 * Qs1;
+    e2.nR_pre = nR2;
+    rc = execute_il(p2, nullptr, N1, InLayout{0, 0, 0, 0}, 0, PDD_PAD_VALUE, pad2vals, out, ld_out,
+                    n_out, row_g, row_d, 0.f, stream, e2);
+  }
+  (void)hipFreeAsync(R2, st);
+  return rc;
 }
 
 int pdd_sweep_set_timing(pdd_sweep_plan* p, int on) {

@@ -31,6 +31,17 @@ def _is_int_pad(padval):
     return float(padval).is_integer() and 0 <= float(padval) <= 255
 
 
+def _pads16(x, C, padval):
+    """(pad mode, per-channel pad values) of a 16-bit sweep."""
+    if isinstance(padval, str):
+        if padval != "rotate":
+            raise ValueError("16-bit sweep input takes integer or 'rotate' pads")
+        return _lib.PAD_ROTATE, None
+    if not (float(padval).is_integer() and 0 <= float(padval) <= 1023):
+        raise ValueError("16-bit sweep pads must be integers in [0, 1023]")
+    return _lib.PAD_VALUE, torch.full((C,), float(padval), dtype=torch.float32, device=x.device)
+
+
 def _is_int_pad16(padval):
     """Pads the 16-bit sweep can bake in exactly (integers <= 1023, 'rotate')."""
     if isinstance(padval, str):
@@ -137,15 +148,7 @@ class DMSweep(object):
                 pv = torch.full((self.C,), float(padval), dtype=torch.float32, device=x.device)
         elif x.dtype in _U16_TYPES:
             code = _lib.U16
-            if isinstance(padval, str):
-                if padval != "rotate":
-                    raise ValueError("16-bit sweep input takes integer or 'rotate' pads")
-                mode, pv = _lib.PAD_ROTATE, None
-            else:
-                if not (float(padval).is_integer() and 0 <= float(padval) <= 1023):
-                    raise ValueError("16-bit sweep pads must be integers in [0, 1023]")
-                mode = _lib.PAD_VALUE
-                pv = torch.full((self.C,), float(padval), dtype=torch.float32, device=x.device)
+            mode, pv = _pads16(x, self.C, padval)
         elif x.dtype == torch.float32:
             code = _lib.F32
             mode, pv = _pad_args(x, padval)
@@ -153,6 +156,26 @@ class DMSweep(object):
             raise TypeError("sweep input must be float32, uint8 or 16-bit")
         call("pdd_sweep_execute_ex", self._plan(code), ptr(x), N, x.stride(0), 0, 0, mode, ptr(pv),
              ptr(out), out.stride(0), n_out, float(out_bias), stream_ptr(stream))
+        return out
+
+    def sweep_ds(self, x8, ds, padval=0, out=None, n_out=None, stream=None):
+        """Sweep ``Spectra.downsample(ds)`` of the 8-bit rows ``x8`` ([C,
+        n_raw] uint8) without forming the downsampled copy: the co-adds (<=
+        1020, exact) are formed by the interleave pre-pass of the 16-bit sweep
+        (pdd_sweep_execute_ds; dtype='u16' plans, ds 2..4).  Pads act on the
+        downsampled series (integers <= 1023 or 'rotate')."""
+        if self.dtype != "u16":
+            raise TypeError("sweep_ds needs a dtype='u16' DMSweep")
+        mode, pv = _pads16(x8, self.C, padval)
+        N = x8.shape[1] // int(ds)
+        n_out = self.n_out(N, True) if n_out is None else int(n_out)
+        if out is None:
+            out = torch.empty((self.D, max(n_out, 1)), dtype=torch.float32, device=x8.device)
+        assert x8.dtype == torch.uint8 and x8.dim() == 2 and x8.shape[0] == self.C
+        assert x8.stride(1) == 1 and out.shape[0] == self.D and out.shape[1] >= n_out
+        assert out.stride(1) == 1
+        call("pdd_sweep_execute_ds", self._plan(_lib.U16), ptr(x8), x8.shape[1], x8.stride(0),
+             int(ds), mode, ptr(pv), ptr(out), out.stride(0), n_out, 0, 1, stream_ptr(stream))
         return out
 
     def sweep_pieces(self, xp, N, piece, x_off, n_out, out, stream=None):
@@ -266,6 +289,20 @@ class GroupedSweep(object):
              ptr(padvals), ptr(out), out.stride(0), n_out, row_g, row_d, stream_ptr(stream))
         return out
 
+    def execute_ds(self, x8, ds, n_out, out, row_g, row_d, pad_mode=_lib.PAD_VALUE, padvals=None,
+                   stream=None):
+        """The grouped sweep of ``x8`` ([n_grp*C, n_raw] uint8) downsampled by
+        ``ds`` (2..4) on the fly (pdd_sweep_execute_ds; dtype='u16' plans)."""
+        assert self.dtype == "u16", "execute_ds needs a dtype='u16' GroupedSweep"
+        assert x8.dtype == torch.uint8 and x8.dim() == 2 and x8.shape[0] == self.n_grp * self.C
+        assert x8.stride(1) == 1
+        if pad_mode == _lib.PAD_VALUE and padvals is None:
+            padvals = torch.zeros(x8.shape[0], dtype=torch.float32, device=x8.device)
+        call("pdd_sweep_execute_ds", self._plan, ptr(x8), x8.shape[1], x8.stride(0), int(ds),
+             pad_mode, ptr(padvals), ptr(out), out.stride(0), n_out, row_g, row_d,
+             stream_ptr(stream))
+        return out
+
     def close(self):
         if self._plan is not None:
             _lib.lib().pdd_sweep_plan_destroy(self._plan)
@@ -328,8 +365,6 @@ class DDplanExecutor(object):
             # co-add is kept as uint16 and swept on the 16-bit path
             s.u16 = bool(raw8) and 1 < s.ds <= 4
             s.x = None      # float32 image of a downsampled step (allocated on use)
-            s.x16 = (torch.empty((self.C, s.n_ds), dtype=torch.int16, device=self.device)
-                     if s.u16 else None)
             calls = step.subband_calls()
             s.two_stage = calls[0][0] is not None
             if not s.two_stage:
@@ -349,8 +384,12 @@ class DDplanExecutor(object):
             t1 = np.stack([_delays.subband_bins(sd, self.freqs, s.dt, nsub, cur_dm=cur_dm)
                            for sd in subdms])                      # [ncall, C]
             s.t1 = t1.reshape(ncall, nsub, cps).transpose(1, 0, 2)  # [nsub, ncall, cps]
-            s.g1 = GroupedSweep(s.t1, "u16" if s.u16 else "f32")
-            s.sub = torch.empty((ncall * nsub, s.n_ds), dtype=torch.float32, device=self.device)
+            # 8-bit rows: stage 1 on the exact integer path (u8 at the raw
+            # rate, u16 co-adds at ds <= 4)
+            s.int1 = "u8" if (raw8 and s.ds == 1) else ("u16" if s.u16 else None)
+            s.g1 = GroupedSweep(s.t1, s.int1 or "f32")
+            s.sub = None    # subband plane (only when the stages are not chained)
+            s.chain, s.chain_pads = True, None
             # stage 2: [ncall groups][per-call DMs][nsub subbands at their centres]
             _, _, ctr = _delays.subband_layout(self.freqs, nsub)
             per = len(calls[0][1])
@@ -376,11 +415,12 @@ class DDplanExecutor(object):
         for s in self.steps:
             # the exact 16-bit path needs the raw 8-bit rows and integer pads
             use16 = s.u16 and raw8 is not None and _is_int_pad16(padval)
+            use8 = (s.two_stage and s.int1 == "u8" and raw8 is not None
+                    and _is_int_pad(padval))
             if s.ds > 1 and use16:
-                x = s.x16
-                if s.n_ds:
-                    call("pdd_downsample_u8_u16", ptr(raw8), self.C, self.N, raw8.stride(0),
-                         s.ds, ptr(x), s.n_ds, stream_ptr())
+                # the 16-bit sweeps co-add the raw rows in their interleave
+                # pre-pass (pdd_sweep_execute_ds): no downsampled copy
+                x = raw8
             elif s.ds > 1:
                 if s.x is None:
                     s.x = torch.empty((self.C, s.n_ds), dtype=torch.float32, device=self.device)
@@ -392,12 +432,16 @@ class DDplanExecutor(object):
                     call("pdd_downsample", ptr(src), self.C, self.N, src.stride(0), s.ds, ptr(x),
                          s.n_ds, stream_ptr())
             else:
-                x = src
+                x = raw8 if use8 else src
             if not s.two_stage:
                 sw = s.sw
                 if sw.dtype == "u8" and raw8 is not None and _is_int_pad(padval):
                     x = raw8
-                elif sw.dtype != "f32" and not (sw.dtype == "u16" and use16):
+                elif sw.dtype == "u16" and use16:
+                    sw.sweep_ds(x, s.ds, padval=padval, out=s.plane, n_out=s.n_out)
+                    results.append((s.step, s.step.DMs, s.plane[:, :s.n_out]))
+                    continue
+                elif sw.dtype != "f32":
                     # pads that are not small integers (or no raw rows): float image
                     if getattr(s, "sw_f32", None) is None:
                         s.sw_f32 = DMSweep(s.step.DMs, self.freqs, s.dt, cur_dm=self.cur_dm,
@@ -407,17 +451,46 @@ class DDplanExecutor(object):
                 results.append((s.step, s.step.DMs, s.plane[:, :s.n_out]))
                 continue
             g1 = s.g1
-            if s.u16 and not use16:
+            if s.int1 and not (use16 or use8):
                 if getattr(s, "g1_f32", None) is None:
                     s.g1_f32 = GroupedSweep(s.t1, "f32")
                 g1 = s.g1_f32
-            if use16:
+            if (use16 or use8) and not isinstance(padval, str) and s.chain:
+                # both stages chained: stage 1 writes stage 2's input image
+                # directly (pdd_subband_chain), no subband plane
+                if s.n_out:
+                    if s.chain_pads is None or s.chain_pads[0] != float(padval):
+                        s.chain_pads = (float(padval),
+                                        torch.full((self.C,), float(padval), dtype=torch.float32,
+                                                   device=self.device),
+                                        torch.full((s.ncall * s.nsub,), float(padval),
+                                                   dtype=torch.float32, device=self.device))
+                    _, pv1, pv2 = s.chain_pads
+                    rc = _lib.lib().pdd_subband_chain(
+                        g1._plan, ptr(raw8), self.N, raw8.stride(0), s.ds, _lib.PAD_VALUE,
+                        ptr(pv1), s.g2._plan, ptr(pv2), ptr(s.plane), s.plane.stride(0),
+                        s.n_out, s.per, 1, stream_ptr())
+                    if rc != -2:
+                        _lib.check(rc, "pdd_subband_chain")
+                        results.append((s.step, s.step.DMs, s.plane[:, :s.n_out]))
+                        continue
+                    # -2: a geometry the chain does not take (nothing was
+                    # launched): run the stages apart from now on
+                    s.chain = False
+            if s.sub is None:
+                s.sub = torch.empty((s.ncall * s.nsub, s.n_ds), dtype=torch.float32,
+                                    device=self.device)
+            if use16 or use8:
                 pv = torch.full((x.shape[0],), float(padval), dtype=torch.float32,
                                 device=x.device) if not isinstance(padval, str) else None
                 mode = _lib.PAD_ROTATE if isinstance(padval, str) else _lib.PAD_VALUE
             else:
                 mode, pv = _pad_args(x, padval)
-            g1(x, s.n_ds, s.sub, row_g=1, row_d=s.nsub, pad_mode=mode, padvals=pv)
+            if use16 and s.ds > 1:
+                g1.execute_ds(x, s.ds, s.n_ds, s.sub, row_g=1, row_d=s.nsub, pad_mode=mode,
+                              padvals=pv)
+            else:
+                g1(x, s.n_ds, s.sub, row_g=1, row_d=s.nsub, pad_mode=mode, padvals=pv)
             if s.n_out:
                 # stage 2 pads: those of each pass's subbanded Spectra
                 # (dedisperse(dm, padval) on the subbanded data)

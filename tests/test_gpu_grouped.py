@@ -127,3 +127,100 @@ def test_executor_u16_steps_and_pads(gpu, padval):
         else:
             np.testing.assert_array_equal(got, ref)
     ex.close()
+
+
+@pytest.mark.parametrize("ds", [2, 3, 4])
+@pytest.mark.parametrize("padval", [0, 17, "rotate"])
+@pytest.mark.parametrize("layout", ["vec16", "vec", "bytes"])
+def test_sweep_ds_fused_downsample(gpu, ds, padval, layout):
+    """pdd_sweep_execute_ds (8-bit rows co-added by ds inside the 16-bit
+    interleave pre-pass) == the oracle's Spectra.downsample + sweep, bit for
+    bit, on a ragged raw length, over the full width (pads/rotation at the
+    edges).  Row layouts: 16-B aligned rows (the 16-byte-load kernel), rows
+    aligned to ds only, and unaligned rows (byte loads).  Grouped plans too."""
+    import torch
+    from pypulsar_amd.sweep import DMSweep, GroupedSweep
+    C, n_raw = 96, (1 << 13) + 3
+    width = {"vec16": 8208, "vec": 8212, "bytes": 8208}[layout]
+    x = u8_data(C, width, 40 + ds)
+    xt = torch.from_numpy(x).cuda()
+    o = 1 if layout == "bytes" else 0
+    x8 = xt[:, o:o + n_raw]
+    ref8 = x[:, o:o + n_raw]
+    freqs = band(C)
+    dms = np.linspace(0.0, 60.0, 37)
+    sw = DMSweep(dms, freqs, DT * ds, dtype="u16")
+    N = n_raw // ds
+    got = sw.sweep_ds(x8, ds, padval=padval, n_out=N).cpu().numpy()
+    xd, _ = orc.downsample(ref8.astype(np.float64), DT, ds)
+    ref = orc.sweep_plane(xd, sw.table, padval=padval, n_out=N)
+    np.testing.assert_array_equal(got, ref)
+    # grouped: two groups of C/2 channels, rows interleaved
+    t2 = np.stack([sw.table[:, :C // 2], sw.table[:, C // 2:]])
+    gs = GroupedSweep(t2, "u16")
+    out = torch.full((2 * len(dms), N), -1.0, device="cuda")
+    mode = 1 if isinstance(padval, str) else 0
+    pv = None if mode else torch.full((C,), float(padval), device="cuda")
+    from pypulsar_amd import _lib
+    gs.execute_ds(x8, ds, N, out, row_g=1, row_d=2,
+                  pad_mode=_lib.PAD_ROTATE if mode else _lib.PAD_VALUE, padvals=pv)
+    g = out.cpu().numpy()
+    for k in range(2):
+        refk = orc.sweep_plane(xd[k * C // 2:(k + 1) * C // 2], t2[k], padval=padval, n_out=N)
+        np.testing.assert_array_equal(g[k::2], refk)
+    sw.close()
+    gs.close()
+
+
+@pytest.mark.parametrize("ds", [1, 2, 4])
+@pytest.mark.parametrize("padval", [0, 9])
+def test_subband_chain_equals_stages(gpu, ds, padval):
+    """pdd_subband_chain (stage 1 writes stage 2's float32 quarters image
+    directly) == stage 1 into a subband plane + stage 2 over it, bit for bit,
+    on a ragged block; and one row against the oracle's Spectra.subband +
+    dedisperse + channel sum.  ds 1: 8-bit stage 1; ds 2/4: co-added on the
+    fly (16-bit stage 1)."""
+    import torch
+    from pypulsar_amd import _lib, delays
+    from pypulsar_amd._lib import ptr
+    from pypulsar_amd.sweep import GroupedSweep
+    C, nsub, n_raw = 128, 8, (1 << 14) + 5 * ds
+    cps = C // nsub
+    freqs = band(C)
+    dt = DT * ds
+    x = u8_data(C, n_raw + 11, 70 + ds)[:, :n_raw].copy()
+    x8 = torch.from_numpy(x).cuda()
+    subdms = [5.0, 15.0, 25.0]
+    dms = [np.linspace(sd - 5, sd + 5, 6, endpoint=False) for sd in subdms]
+    t1 = np.stack([delays.subband_bins(sd, freqs, dt, nsub) for sd in subdms])
+    t1 = t1.reshape(len(subdms), nsub, cps).transpose(1, 0, 2)
+    g1 = GroupedSweep(t1, "u8" if ds == 1 else "u16")
+    _, _, ctr = delays.subband_layout(freqs, nsub)
+    t2 = np.stack([delays.sweep_table(d, ctr, dt) for d in dms])
+    g2 = GroupedSweep(t2, "f32")
+    N = n_raw // ds
+    n_out = N - int(t2.max())
+    pv1 = torch.full((C,), float(padval), device="cuda")
+    pv2 = torch.full((len(subdms) * nsub,), float(padval), device="cuda")
+    # stages apart
+    sub = torch.empty((len(subdms) * nsub, N), device="cuda")
+    if ds == 1:
+        g1(x8, N, sub, row_g=1, row_d=nsub, pad_mode=_lib.PAD_VALUE, padvals=pv1)
+    else:
+        g1.execute_ds(x8, ds, N, sub, row_g=1, row_d=nsub, pad_mode=_lib.PAD_VALUE, padvals=pv1)
+    ref = torch.full((len(subdms) * 6, n_out), -1.0, device="cuda")
+    g2(sub, n_out, ref, row_g=6, row_d=1, pad_mode=_lib.PAD_VALUE, padvals=pv2)
+    got = torch.full_like(ref, -2.0)
+    _lib.call("pdd_subband_chain", g1._plan, ptr(x8), n_raw, x8.stride(0), ds, _lib.PAD_VALUE,
+              ptr(pv1), g2._plan, ptr(pv2), ptr(got), got.stride(0), n_out, 6, 1,
+              _lib.stream_ptr())
+    got = got.cpu().numpy()
+    np.testing.assert_array_equal(got, ref.cpu().numpy())
+    # oracle: pass 1, DM 2 -> Spectra.downsample + subband + dedisperse + sum
+    xd, _ = orc.downsample(x.astype(np.float64), DT, ds)
+    subd, sfreqs = orc.subband(xd, freqs, dt, nsub, subdm=subdms[1], padval=padval)
+    ded, _ = orc.dedisperse(subd, sfreqs, dt, dms[1][2], cur_dm=0.0, padval=padval)
+    want = orc.channel_sum(ded)
+    np.testing.assert_array_equal(got[6 + 2], want[:n_out])
+    g1.close()
+    g2.close()
