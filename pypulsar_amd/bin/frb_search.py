@@ -23,15 +23,16 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
-def _chunks(fb, block, nbuf=4):
-    """Pinned [n, nchans] host chunks of the file, in rotation (a buffer is
-    reused nbuf chunks later, after its asynchronous copy has completed:
-    StreamingSweep keeps at most 2 chunks in flight)."""
+def _chunks(fb, block, nbuf=4, start_block=0):
+    """Pinned [n, nchans] host chunks of the file from block ``start_block``
+    on, in rotation (a buffer is reused nbuf chunks later, after its
+    asynchronous copy has completed: StreamingSweep keeps at most 2 chunks in
+    flight)."""
     import torch
     tdt = {np.dtype(np.uint8): torch.uint8, np.dtype(np.uint16): torch.int16,
            np.dtype(np.float32): torch.float32}[np.dtype(fb.dtype)]
     bufs = [torch.empty((block, fb.nchans), dtype=tdt, pin_memory=True) for _ in range(nbuf)]
-    done, i = 0, 0
+    done, i = int(start_block) * block, 0
     while done < fb.number_of_samples:
         h = bufs[i % nbuf]
         n = fb.read_block_into(done, h.numpy().view(np.dtype(fb.dtype))[:block])

@@ -131,16 +131,21 @@ class StreamingSweep(object):
         self.sweep(self.img[:, :nd], trim=True, out=out, out_bias=-float(self.offset * self.C))
         return out[:, :n_out]
 
-    def __call__(self, chunks, planes=None):
+    def __call__(self, chunks, planes=None, start_block=0):
         """chunks: iterable of host tensors [n, C] (pinned for an asynchronous
         copy; every chunk but the last must hold exactly ``block`` spectra).
         planes: optional list of preallocated [D, block/ds] device planes,
         used in rotation by EMITTED-block count (block j -> planes[j % len]),
         so a consumer holding the last len(planes) - 1 planes never sees them
-        overwritten.  Yields (t0, plane)."""
+        overwritten.  Yields (t0, plane).
+
+        Restart by block index: a block's plane depends only on its own chunk
+        and the head of the next one, so a run resumed at block k -- chunks
+        k, k+1, ... of the stream and ``start_block=k`` -- yields exactly the
+        (t0, plane) pairs of blocks k, k+1, ... of the uninterrupted run."""
         cur = torch.cuda.current_stream(self.device)
         prev = None  # (buffer index, n spectra)
-        t0 = 0
+        t0 = int(start_block) * self.n_out_block
         i = -1
         emitted = 0
         for i, chunk in enumerate(chunks):

@@ -117,3 +117,26 @@ def test_stream_equals_one_shot(gpu, nchunks, last, zdm):
     ref = orc.sweep_plane(orc.zdm_downsample(x, ds), orc.sweep_table(dms, freqs, DT * ds))
     assert rel_err(got, ref) <= 1e-5
     st.close()
+
+
+@pytest.mark.parametrize("zdm", ["int", "float"])
+def test_stream_restart_by_block_index(gpu, zdm):
+    """A stream resumed at block k (chunks k.., start_block=k) yields exactly
+    the (t0, plane) pairs of blocks k.. of the uninterrupted run."""
+    import torch
+    from pypulsar_amd.stream import StreamingSweep
+    C, block, ds = 96, 4096, 2
+    freqs = band(C)
+    dms = np.linspace(0.0, 200.0, 40)
+    N = block * 4 + 1000
+    x = u8_data(N, C, 23)
+    st = StreamingSweep(dms, freqs, DT, block=block, downsamp=ds, zero_dm=zdm)
+    chunks = [torch.from_numpy(x[i:i + block]).pin_memory() for i in range(0, N, block)]
+    full = [(t0, p.cpu().numpy()) for t0, p in st(chunks)]
+    for k in (1, 3):
+        part = [(t0, p.cpu().numpy()) for t0, p in st(chunks[k:], start_block=k)]
+        assert len(part) == len(full) - k
+        for (ta, pa), (tb, pb) in zip(part, full[k:]):
+            assert ta == tb
+            np.testing.assert_array_equal(pa, pb)
+    st.close()
