@@ -44,6 +44,10 @@ enum { PDD_LAYOUT_TIME_MAJOR = 0, /* [nspec][nchan], filterbank file order */
 
 int pdd_version(void);
 const char* pdd_last_error(void);
+/* Free the device scratch the library keeps per stream (sweep images,
+ * partial sums); synchronises the device.  Optional: the next call that
+ * needs scratch allocates it again. */
+int pdd_scratch_release(void);
 /* hipStreamSynchronize(stream) */
 int pdd_sync(void* stream);
 

@@ -35,7 +35,7 @@ EXPORTS = (
     "pdd_sweep_plan_create_grouped", "pdd_sweep_execute_grouped", "pdd_sp_chunk_stats",
     "pdd_sp_search", "pdd_psrfits_subints", "pdd_downsample_u8", "pdd_sweep_timing_read",
     "pdd_sweep_execute_ex", "pdd_zdm_int_downsample", "pdd_downsample_u8_u16",
-    "pdd_sweep_execute_ds", "pdd_subband_chain",
+    "pdd_sweep_execute_ds", "pdd_subband_chain", "pdd_scratch_release",
 )
 
 
@@ -54,6 +54,7 @@ _SIGS = {
     "pdd_version": ([], _int),
     "pdd_last_error": ([], ctypes.c_char_p),
     "pdd_sync": ([_vp], _int),
+    "pdd_scratch_release": ([], _int),
     "pdd_corner_turn": ([_vp, _int, _i64, _i64, _i64, _vp, _int, _i64, _vp], _int),
     "pdd_convert_f32": ([_vp, _int, _i64, _i64, _i64, _vp, _i64, _vp], _int),
     "pdd_channel_stats": ([_vp, _i64, _i64, _i64, _int, _vp, _vp], _int),

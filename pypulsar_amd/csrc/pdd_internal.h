@@ -42,6 +42,17 @@ void set_error(const char* fmt, ...);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Device scratch owned by the library, one buffer per (stream, slot), grown
+// with hipMalloc and kept for reuse.  Work on one stream is ordered, so
+// consecutive calls on the same stream share a slot safely; a call that
+// needs two buffers at once uses two slots.  (Replaces stream-ordered
+// hipMallocAsync/hipFreeAsync, whose pool pages, released at device
+// synchronisation, were seen to alias live hipMalloc buffers -- wrong sweep
+// results in tests/native/abi_asan.cpp.)  Returns nullptr and sets the error
+// message on failure.
+enum { kScratchImage = 0, kScratchChain = 1, kScratchPartial = 2, kScratchSmall = 3 };
+void* scratch(hipStream_t st, int slot, size_t bytes);
+
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Value of channel row `row` at sample s, with the reference pad semantics

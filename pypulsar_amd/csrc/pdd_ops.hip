@@ -8,6 +8,8 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 #include "pdd_internal.h"
 
@@ -20,6 +22,47 @@ void set_error(const char* fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
+}
+
+namespace {
+struct ScratchBuf {
+  hipStream_t st;
+  int slot;
+  void* ptr;
+  size_t bytes;
+};
+std::mutex g_scratch_mu;
+std::vector<ScratchBuf> g_scratch;
+}  // namespace
+
+void* scratch(hipStream_t st, int slot, size_t bytes) {
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  bytes = std::max<size_t>(bytes, 256);
+  for (auto& b : g_scratch) {
+    if (b.st != st || b.slot != slot) continue;
+    if (b.bytes >= bytes) return b.ptr;
+    // grow: the stream's queued work may still read the old buffer
+    hipError_t e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = hipFree(b.ptr);
+    b.ptr = nullptr;
+    b.bytes = 0;
+    if (e == hipSuccess) e = hipMalloc(&b.ptr, bytes);
+    if (e != hipSuccess) {
+      b.ptr = nullptr;
+      set_error("device scratch (%zu bytes): %s", bytes, hipGetErrorString(e));
+      return nullptr;
+    }
+    b.bytes = bytes;
+    return b.ptr;
+  }
+  void* p = nullptr;
+  const hipError_t e = hipMalloc(&p, bytes);
+  if (e != hipSuccess) {
+    set_error("device scratch (%zu bytes): %s", bytes, hipGetErrorString(e));
+    return nullptr;
+  }
+  g_scratch.push_back({st, slot, p, bytes});
+  return p;
 }
 
 // ---------------------------------------------------------------- loaders
@@ -1001,6 +1044,15 @@ int pdd_version(void) { return 1; }
 
 const char* pdd_last_error(void) { return pdd::g_err; }
 
+int pdd_scratch_release(void) {
+  std::lock_guard<std::mutex> lock(pdd::g_scratch_mu);
+  PDD_HIP(hipDeviceSynchronize());
+  for (auto& b : pdd::g_scratch)
+    if (b.ptr) (void)hipFree(b.ptr);
+  pdd::g_scratch.clear();
+  return 0;
+}
+
 int pdd_sync(void* stream) {
   PDD_HIP(hipStreamSynchronize(as_stream(stream)));
   return 0;
@@ -1133,14 +1185,16 @@ int pdd_shift_group_sum(const float* x, int64_t C, int64_t N, int64_t ld, const 
   PDD_REQUIRE(csplit * nsub * tiles < (1ll << 31), "pdd_shift_group_sum: too large");
   hipStream_t st = as_stream(stream);
   double* part = nullptr;
-  if (csplit > 1)
-    PDD_HIP(hipMallocAsync((void**)&part, (size_t)(csplit * nsub * n_out) * sizeof(double), st));
+  if (csplit > 1) {
+    part = static_cast<double*>(
+        scratch(st, kScratchPartial, (size_t)(csplit * nsub * n_out) * sizeof(double)));
+    if (!part) return -2;
+  }
   k_shift_group_sum<<<(unsigned)(csplit * nsub * tiles), kGsWaves * 64, 0, st>>>(
       x, N, ld, bins, pad_mode, padvals, cps, csplit, out, part, ld_out, n_out, tiles, nsub);
   if (csplit > 1) {
     k_group_sum_reduce<<<(unsigned)cdiv(nsub * n_out, 256), 256, 0, st>>>(part, csplit, nsub,
                                                                           n_out, out, ld_out);
-    (void)hipFreeAsync(part, st);
   }
   PDD_LAUNCHED();
   return 0;
@@ -1261,15 +1315,14 @@ int pdd_global_stats(const float* x, int64_t C, int64_t N, int64_t ld, float* ou
   PDD_REQUIRE(x && out4, "pdd_global_stats: null pointer");
   PDD_REQUIRE(C > 0 && N > 0 && ld >= N, "pdd_global_stats: bad shape");
   hipStream_t s = as_stream(stream);
-  double* scratch = nullptr;
-  PDD_HIP(hipMallocAsync((void**)&scratch, (kGlobBlocks * 3 + 1) * sizeof(double), s));
-  double* fin = scratch + kGlobBlocks * 3;
-  k_global_partial<<<kGlobBlocks, 256, 0, s>>>(x, C, N, ld, 0, fin, scratch);
-  k_global_reduce<<<1, 256, 0, s>>>(scratch, 0, C * N, fin, out4);
-  k_global_partial<<<kGlobBlocks, 256, 0, s>>>(x, C, N, ld, 1, fin, scratch);
-  k_global_reduce<<<1, 256, 0, s>>>(scratch, 1, C * N, fin, out4);
+  double* part = static_cast<double*>(scratch(s, kScratchSmall, (kGlobBlocks * 3 + 1) * sizeof(double)));
+  if (!part) return -2;
+  double* fin = part + kGlobBlocks * 3;
+  k_global_partial<<<kGlobBlocks, 256, 0, s>>>(x, C, N, ld, 0, fin, part);
+  k_global_reduce<<<1, 256, 0, s>>>(part, 0, C * N, fin, out4);
+  k_global_partial<<<kGlobBlocks, 256, 0, s>>>(x, C, N, ld, 1, fin, part);
+  k_global_reduce<<<1, 256, 0, s>>>(part, 1, C * N, fin, out4);
   const hipError_t e = hipGetLastError();
-  (void)hipFreeAsync(scratch, s);
   PDD_REQUIRE(e == hipSuccess, "pdd_global_stats: launch failed: %s", hipGetErrorString(e));
   return 0;
 }
@@ -1333,7 +1386,10 @@ int pdd_zdm_downsample(const void* in, int dtype, int64_t nspec, int64_t nchan, 
   if (nspec < factor) return 0;
   hipStream_t s = as_stream(stream);
   double* mean = nullptr;
-  if (zero_dm) PDD_HIP(hipMallocAsync((void**)&mean, (size_t)nspec * sizeof(double), s));
+  if (zero_dm) {
+    mean = static_cast<double*>(scratch(s, kScratchSmall, (size_t)nspec * sizeof(double)));
+    if (!mean) return -2;
+  }
   const int64_t tiles_c = cdiv(nchan, 64);
   const int64_t blocks = cdiv(nspec, 64) * tiles_c;
   PDD_REQUIRE(blocks < (1ll << 31), "pdd_zdm_downsample: too large");
@@ -1367,7 +1423,6 @@ int pdd_zdm_downsample(const void* in, int dtype, int64_t nspec, int64_t nchan, 
 #undef ZD
 #undef ZV
   const hipError_t e = hipGetLastError();
-  if (mean) (void)hipFreeAsync(mean, s);
   PDD_REQUIRE(e == hipSuccess, "pdd_zdm_downsample: launch failed: %s", hipGetErrorString(e));
   return 0;
 }
@@ -1392,7 +1447,8 @@ int pdd_zdm_int_downsample(const void* in, int dtype, int64_t nspec, int64_t nch
   hipStream_t s = as_stream(stream);
   double* mean = nullptr;
   if (mode != PDD_ZDM_NONE) {
-    PDD_HIP(hipMallocAsync((void**)&mean, (size_t)nspec * sizeof(double), s));
+    mean = static_cast<double*>(scratch(s, kScratchSmall, (size_t)nspec * sizeof(double)));
+    if (!mean) return -2;
     k_spectrum_mean_vec<uint8_t><<<(unsigned)cdiv(nspec, 4), 256, 0, s>>>(
         (const uint8_t*)in, nspec, nchan, ld, mean);
   }
@@ -1410,7 +1466,6 @@ int pdd_zdm_int_downsample(const void* in, int dtype, int64_t nspec, int64_t nch
     k_zdm_int_ds_vec<2><<<grid, 256, 0, s>>>(x, nchan, ld, mean, (int)factor, out, ld_out, nout,
                                              tcv, offset);
   const hipError_t e = hipGetLastError();
-  if (mean) (void)hipFreeAsync(mean, s);
   PDD_REQUIRE(e == hipSuccess, "pdd_zdm_int_downsample: launch failed: %s", hipGetErrorString(e));
   return 0;
 }

@@ -1693,7 +1693,8 @@ static int execute_mx(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
   const int64_t nR8_alloc = (seg + extra + 15) / 16 * 16;
   uint8_t* R8 = nullptr;
   hipStream_t st = as_stream(stream);
-  PDD_HIP(hipMallocAsync((void**)&R8, (size_t)(Cpad * nR8_alloc), st));
+  R8 = static_cast<uint8_t*>(scratch(st, kScratchImage, (size_t)(Cpad * nR8_alloc)));
+  if (!R8) return -2;
   sweep_mx_fn kf = mx_kernel_for(p->v);
   int rc = kf ? 0 : -1;
   for (int64_t t_base = 0; t_base < n_out && rc == 0; t_base += seg) {
@@ -1722,7 +1723,6 @@ static int execute_mx(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t
       pm->timed++;
     }
   }
-  (void)hipFreeAsync(R8, st);
   if (rc == -1) set_error("pdd_sweep_execute: grid too large or no MFMA kernel");
   if (rc == -3) set_error("pdd_sweep_execute: kernel launch failed");
   return rc;
@@ -1788,8 +1788,10 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
   float4* R = nullptr;
   hipStream_t st = as_stream(stream);
   // C rows of the image + one row of zeros (the u16 kernel's pad channel)
-  if (!ex.R_pre)
-    PDD_HIP(hipMallocAsync((void**)&R, (size_t)((C + 1) * nr_alloc) * sizeof(float4), st));
+  if (!ex.R_pre) {
+    R = static_cast<float4*>(scratch(st, kScratchImage, (size_t)((C + 1) * nr_alloc) * sizeof(float4)));
+    if (!R) return -2;
+  }
   const int dbg = debug_flags();
   int rc = 0;
   for (int64_t t_base = 0; t_base < n_out && rc == 0; t_base += seg) {
@@ -1859,7 +1861,6 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
       pm->timed++;
     }
   }
-  if (R) (void)hipFreeAsync(R, st);
   if (rc == -4) set_error("pdd_subband_chain: stage-2 image geometry mismatch");
   if (rc == -1) set_error("pdd_sweep_execute: grid too large");
   if (rc == -3) set_error("pdd_sweep_execute: kernel launch failed");
@@ -2208,7 +2209,8 @@ int pdd_subband_chain(const pdd_sweep_plan* p1, const void* x, int64_t n_raw, in
   const int64_t nR2 = 2 * Qs1 + ov;
   float4* R2 = nullptr;
   hipStream_t st = as_stream(stream);
-  PDD_HIP(hipMallocAsync((void**)&R2, (size_t)(C2 * nR2) * sizeof(float4), st));
+  R2 = static_cast<float4*>(scratch(st, kScratchChain, (size_t)(C2 * nR2) * sizeof(float4)));
+  if (!R2) return -2;
   IlExtra e1;
   e1.ds = (int)ds;
   e1.r2_pad = pad2vals;
@@ -2225,7 +2227,6 @@ int pdd_subband_chain(const pdd_sweep_plan* p1, const void* x, int64_t n_raw, in
     rc = execute_il(p2, nullptr, N1, InLayout{0, 0, 0, 0}, 0, PDD_PAD_VALUE, pad2vals, out, ld_out,
                     n_out, row_g, row_d, 0.f, stream, e2);
   }
-  (void)hipFreeAsync(R2, st);
   return rc;
 }
 

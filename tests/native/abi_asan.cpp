@@ -1,0 +1,168 @@
+// Host-AddressSanitizer driver for libpdd's C ABI (sanitizer
+// build of the host code).  Built by scripts/asan_check.sh with the host
+// side instrumented (-Xarch_host -fsanitize=address; device code untouched)
+// and run on the GPU box.  It drives the host logic behind include/pdd.h --
+// argument checks, sweep-plan table/chunk building, grouped plans, timing
+// pools, create/destroy cycles -- on small random grids, and checks every
+// sweep against a plain host sum:
+//     plane[d][t] = sum_c X(c, t + table[d][c])   (pad 0 outside [0, N))
+// Exit status 0 = all checks passed and no ASan report.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "pdd.h"
+
+static int failures = 0;
+#define CHECK(cond, ...)                                   \
+  do {                                                     \
+    if (!(cond)) {                                         \
+      std::fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+      std::fprintf(stderr, __VA_ARGS__);                   \
+      std::fprintf(stderr, "\n");                          \
+      ++failures;                                          \
+    }                                                      \
+  } while (0)
+
+static void hip_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) {
+    std::fprintf(stderr, "%s: %s\n", what, hipGetErrorString(e));
+    std::exit(2);
+  }
+}
+
+// one sweep of a random [C][N] 8-bit block over a random table, f32 or u8
+static void sweep_case(std::mt19937& rng, int64_t C, int64_t N, int64_t D, int span, int dtype,
+                       bool timing) {
+  std::vector<int32_t> tab((size_t)(D * C));
+  std::uniform_int_distribution<int> sh(0, span);
+  for (int64_t d = 0; d < D; ++d)
+    for (int64_t c = 0; c < C; ++c)  // grows with d like a DM grid, jittered
+      tab[(size_t)(d * C + c)] = (int32_t)((d * span) / std::max<int64_t>(1, D) * (C - c) / C + sh(rng) % 2);
+  int mx = 0;
+  for (int v : tab) mx = std::max(mx, v);
+  const int64_t n_out = std::max<int64_t>(0, N - mx);
+  std::vector<uint8_t> x8((size_t)(C * N));
+  for (auto& v : x8) v = (uint8_t)(rng() & 255);
+  std::vector<float> xf(x8.begin(), x8.end());
+
+  pdd_sweep_plan* plan = nullptr;
+  int rc = pdd_sweep_plan_create(tab.data(), D, C, dtype, &plan);
+  CHECK(rc == 0 && plan, "plan_create C=%lld D=%lld span=%d dtype=%d: rc=%d %s", (long long)C,
+        (long long)D, span, dtype, rc, pdd_last_error());
+  if (rc != 0) return;
+  int64_t info[8] = {0};
+  CHECK(pdd_sweep_plan_info(plan, info) == 0 && info[0] == D && info[1] == C, "plan_info");
+  if (timing) CHECK(pdd_sweep_set_timing(plan, 1) == 0, "set_timing");
+
+  const size_t in_bytes = (size_t)(C * N) * (dtype == PDD_F32 ? 4 : 1);
+  void* dx = nullptr;
+  float *dout = nullptr, *dpad = nullptr;
+  const int64_t ld_out = std::max<int64_t>(1, n_out);
+  hip_ok(hipMalloc(&dx, std::max<size_t>(in_bytes, 16)), "hipMalloc x");
+  hip_ok(hipMalloc(&dout, (size_t)(D * ld_out) * 4), "hipMalloc out");
+  hip_ok(hipMalloc(&dpad, (size_t)C * 4), "hipMalloc pads");
+  hip_ok(hipMemcpy(dx, dtype == PDD_F32 ? (const void*)xf.data() : (const void*)x8.data(), in_bytes,
+                   hipMemcpyHostToDevice), "H2D x");
+  hip_ok(hipMemset(dpad, 0, (size_t)C * 4), "pads");
+  rc = pdd_sweep_execute(plan, dx, N, N, PDD_PAD_VALUE, dpad, dout, ld_out, n_out, nullptr);
+  CHECK(rc == 0, "execute: %s", pdd_last_error());
+  hip_ok(hipDeviceSynchronize(), "sync");
+  std::vector<float> got((size_t)(D * ld_out));
+  hip_ok(hipMemcpy(got.data(), dout, got.size() * 4, hipMemcpyDeviceToHost), "D2H");
+  int bad = 0;
+  for (int64_t d = 0; d < D && bad < 5; ++d)
+    for (int64_t t = 0; t < n_out && bad < 5; ++t) {
+      double s = 0;
+      for (int64_t c = 0; c < C; ++c) {
+        const int64_t k = t + tab[(size_t)(d * C + c)];
+        if (k >= 0 && k < N) s += x8[(size_t)(c * N + k)];
+      }
+      if ((double)got[(size_t)(d * ld_out + t)] != s) {
+        ++bad;
+        CHECK(false, "C=%lld N=%lld D=%lld span=%d dtype=%d variant=%lld max=%d: plane[%lld][%lld] = %g, want %g",
+              (long long)C, (long long)N, (long long)D, span, dtype, (long long)info[7], mx, (long long)d, (long long)t,
+              (double)got[(size_t)(d * ld_out + t)], s);
+      }
+    }
+  if (timing) {
+    float ms = -1;
+    int64_t launches = -1;
+    // a plan whose launches were not bracketed (generic kernel, empty plane)
+    // reports "no timed launch"
+    const int rt = pdd_sweep_timing_read(plan, &ms, &launches);
+    CHECK((rt == 0 && launches >= 1 && ms >= 0) ||
+              (rt != 0 && std::strstr(pdd_last_error(), "no timed launch")),
+          "timing_read: rc %d, %lld launches: %s", rt, (long long)launches, pdd_last_error());
+  }
+  if (std::getenv("ABI_VERBOSE"))
+    std::printf("case C=%lld N=%lld D=%lld span=%d dtype=%d timing=%d variant=%lld lds=%lld "
+                "n_out=%lld bad=%d\n", (long long)C, (long long)N, (long long)D, span, dtype,
+                (int)timing, (long long)info[7], (long long)info[4], (long long)n_out, bad);
+  CHECK(pdd_sweep_plan_destroy(plan) == 0, "destroy");
+  hip_ok(hipFree(dx), "free");
+  hip_ok(hipFree(dout), "free");
+  hip_ok(hipFree(dpad), "free");
+}
+
+int main() {
+  int ndev = 0;
+  hip_ok(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+  CHECK(pdd_version() >= 1, "version");
+
+  // argument checks: errors come back as status codes with a message
+  pdd_sweep_plan* p = nullptr;
+  int32_t t1[4] = {0, 1, 2, 3};
+  CHECK(pdd_sweep_plan_create(nullptr, 1, 4, PDD_F32, &p) != 0 && std::strlen(pdd_last_error()),
+        "null table accepted");
+  CHECK(pdd_sweep_plan_create(t1, 0, 4, PDD_F32, &p) != 0, "D = 0 accepted");
+  CHECK(pdd_sweep_plan_create(t1, 1, 4, 7, &p) != 0, "bad dtype accepted");
+  CHECK(pdd_sweep_plan_create_grouped(t1, 0, 1, 4, PDD_F32, &p) != 0, "0 groups accepted");
+  CHECK(pdd_sweep_execute(nullptr, nullptr, 1, 1, 0, nullptr, nullptr, 1, 1, nullptr) != 0,
+        "null plan executed");
+  CHECK(pdd_sweep_plan_destroy(nullptr) == 0 || std::strlen(pdd_last_error()), "destroy(null)");
+
+  // random grids through every tiling rung the plan can pick
+  std::mt19937 rng(1234);
+  const int64_t Cs[] = {1, 7, 64, 96};
+  const int64_t Ns[] = {1, 300, 5000};
+  const int64_t Ds[] = {1, 5, 57, 130};
+  const int spans[] = {0, 40, 900, 5000};
+  int cases = 0;
+  if (const char* one = std::getenv("ABI_ONE_CASE")) {  // "C,N,D,span,dtype,repeats"
+    long long C, N, D;
+    int span, dtype, reps;
+    if (std::sscanf(one, "%lld,%lld,%lld,%d,%d,%d", &C, &N, &D, &span, &dtype, &reps) == 6) {
+      for (int r = 0; r < reps; ++r) sweep_case(rng, C, N, D, span, dtype, (r & 1) != 0);
+      std::printf("abi_asan: one case x %d, %d failures\n", reps, failures);
+      return failures ? 1 : 0;
+    }
+  }
+  for (int64_t C : Cs)
+    for (int64_t N : Ns)
+      for (int64_t D : Ds)
+        for (int span : spans)
+          for (int dtype : {PDD_F32, PDD_U8}) {
+            if ((rng() & 3) != 0) continue;  // a quarter of the cross product
+            sweep_case(rng, C, N, D, span, dtype, (cases & 1) != 0);
+            ++cases;
+          }
+
+  // grouped plans: create / info / destroy
+  for (int rep = 0; rep < 20; ++rep) {
+    const int64_t G = 1 + rep % 4, D = 3 + rep, C = 8 + 8 * (rep % 3);
+    std::vector<int32_t> tab((size_t)(G * D * C));
+    for (size_t i = 0; i < tab.size(); ++i) tab[i] = (int32_t)(i % 97);
+    pdd_sweep_plan* q = nullptr;
+    const int rc = pdd_sweep_plan_create_grouped(tab.data(), G, D, C, rep % 2 ? PDD_U8 : PDD_F32, &q);
+    CHECK(rc == 0 && q, "grouped create rep %d: %s", rep, pdd_last_error());
+    if (q) CHECK(pdd_sweep_plan_destroy(q) == 0, "grouped destroy");
+  }
+  std::printf("abi_asan: %d sweep cases, %d failures\n", cases, failures);
+  return failures ? 1 : 0;
+}
