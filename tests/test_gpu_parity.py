@@ -478,3 +478,33 @@ def test_sweep_pieces_layout_and_offset(gpu, dtype):
         sw.sweep_pieces(xp, N, P, x_off, cols, out)
         assert torch.equal(out, full[:, x_off:x_off + cols]), (x_off, cols)
     sw.close()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "u8"])
+def test_sweep_two_streams_interleaved(gpu, dtype):
+    """One plan swept on two streams at once, with differently sized blocks
+    alternating (the library's scratch is per stream and grows on demand):
+    every plane equals the single-stream plane of its block."""
+    import torch
+    from pypulsar_amd.sweep import DMSweep
+    C = 96
+    freqs = band(C)
+    dms = np.linspace(0.0, 300.0, 61)
+    sw = DMSweep(dms, freqs, DT, dtype=dtype)
+    rng = np.random.default_rng(31)
+    blocks = [rng.integers(0, 256, size=(C, n), dtype=np.uint8) for n in (9000, 20000, 13000, 30000)]
+    tdt = torch.uint8 if dtype == "u8" else torch.float32
+    xs = [torch.from_numpy(b).cuda().to(tdt) for b in blocks]
+    want = [sw(x).cpu().numpy() for x in xs]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    outs = []
+    for rep in range(3):
+        for i, x in enumerate(xs):
+            st = streams[(i + rep) % 2]
+            with torch.cuda.stream(st):
+                outs.append((i, sw(x, stream=st)))
+    torch.cuda.synchronize()
+    for i, p in outs:
+        np.testing.assert_array_equal(p.cpu().numpy(), want[i])
+    sw.close()
