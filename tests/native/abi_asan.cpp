@@ -9,6 +9,8 @@
 // Exit status 0 = all checks passed and no ASan report.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -110,6 +112,118 @@ static void sweep_case(std::mt19937& rng, int64_t C, int64_t N, int64_t D, int s
   hip_ok(hipFree(dpad), "free");
 }
 
+// single-DM ops of include/pdd.h on small random blocks, against host loops;
+// they share the library's per-stream scratch with the sweeps (partial sums,
+// spectrum means, global statistics)
+template <typename T>
+static T* dev_copy(const std::vector<T>& h) {
+  T* d = nullptr;
+  hip_ok(hipMalloc(&d, std::max<size_t>(h.size() * sizeof(T), 16)), "hipMalloc");
+  if (!h.empty()) hip_ok(hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice), "H2D");
+  return d;
+}
+template <typename T>
+static std::vector<T> host_copy(const T* d, size_t n) {
+  std::vector<T> h(n);
+  hip_ok(hipDeviceSynchronize(), "sync");
+  if (n) hip_ok(hipMemcpy(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost), "D2H");
+  return h;
+}
+
+static void ops_case(std::mt19937& rng, int64_t C, int64_t N) {
+  std::vector<uint8_t> x8((size_t)(C * N));  // time-major [N][C] for the prologues
+  for (auto& v : x8) v = (uint8_t)(rng() & 255);
+  // corner turn u8 [N][C] -> f32 [C][N]
+  uint8_t* dx8 = dev_copy(x8);
+  float* dcm = nullptr;
+  hip_ok(hipMalloc(&dcm, (size_t)(C * N) * 4), "hipMalloc");
+  CHECK(pdd_corner_turn(dx8, PDD_U8, N, C, C, dcm, PDD_F32, N, nullptr) == 0, "corner_turn: %s",
+        pdd_last_error());
+  std::vector<float> cm = host_copy(dcm, (size_t)(C * N));
+  int bad = 0;
+  for (int64_t c = 0; c < C; ++c)
+    for (int64_t t = 0; t < N; ++t)
+      bad += cm[(size_t)(c * N + t)] != (float)x8[(size_t)(t * C + c)];
+  CHECK(bad == 0, "corner_turn C=%lld N=%lld: %d mismatches", (long long)C, (long long)N, bad);
+  // shift + group sum (nsub 1 and C/4), value pads 7, shifts in [-40, 200]
+  std::vector<int32_t> bins((size_t)C);
+  for (auto& b : bins) b = (int32_t)(rng() % 241) - 40;
+  int32_t* dbins = dev_copy(bins);
+  std::vector<float> pads((size_t)C, 7.f);
+  float* dpads = dev_copy(pads);
+  for (int64_t nsub : {(int64_t)1, C / 4}) {
+    if (nsub < 1 || C % nsub) continue;
+    const int64_t n_out = std::max<int64_t>(1, N - 200);
+    float* dout = nullptr;
+    hip_ok(hipMalloc(&dout, (size_t)(nsub * n_out) * 4), "hipMalloc");
+    CHECK(pdd_shift_group_sum(dcm, C, N, N, dbins, PDD_PAD_VALUE, dpads, nsub, dout, n_out, n_out,
+                              nullptr) == 0, "shift_group_sum: %s", pdd_last_error());
+    std::vector<float> got = host_copy(dout, (size_t)(nsub * n_out));
+    const int64_t cps = C / nsub;
+    int badg = 0;
+    for (int64_t k = 0; k < nsub; ++k)
+      for (int64_t t = 0; t < n_out; ++t) {
+        double sum = 0;
+        for (int64_t c = k * cps; c < (k + 1) * cps; ++c) {
+          const int64_t u = t + bins[(size_t)c];
+          sum += (u >= 0 && u < N) ? (double)x8[(size_t)(u * C + c)] : 7.0;
+        }
+        badg += (double)got[(size_t)(k * n_out + t)] != sum;
+      }
+    CHECK(badg == 0, "shift_group_sum C=%lld N=%lld nsub=%lld: %d mismatches", (long long)C,
+          (long long)N, (long long)nsub, badg);
+    hip_ok(hipFree(dout), "free");
+  }
+  // exact integer zero-DM + downsample by 2 (offset 510) of the time-major block
+  if (C % 16 == 0 && N >= 2) {
+    const int64_t f = 2, nout = N / f;
+    uint16_t* dz = nullptr;
+    hip_ok(hipMalloc(&dz, (size_t)(C * nout) * 2), "hipMalloc");
+    CHECK(pdd_zdm_int_downsample(dx8, PDD_U8, N, C, C, f, PDD_ZDM_INT, 510, dz, nout, nullptr) == 0,
+          "zdm_int_downsample: %s", pdd_last_error());
+    std::vector<uint16_t> z = host_copy(dz, (size_t)(C * nout));
+    std::vector<double> m((size_t)N);
+    for (int64_t t = 0; t < N; ++t) {
+      double sum = 0;
+      for (int64_t c = 0; c < C; ++c) sum += x8[(size_t)(t * C + c)];
+      m[(size_t)t] = std::nearbyint(sum / (double)C);  // round half to even
+    }
+    int badz = 0;
+    for (int64_t c = 0; c < C; ++c)
+      for (int64_t j = 0; j < nout; ++j) {
+        double v = 510;
+        for (int64_t k = 0; k < f; ++k) v += (double)x8[(size_t)((j * f + k) * C + c)] - m[(size_t)(j * f + k)];
+        badz += (double)z[(size_t)(c * nout + j)] != v;
+      }
+    CHECK(badz == 0, "zdm_int_downsample C=%lld N=%lld: %d mismatches", (long long)C,
+          (long long)N, badz);
+    hip_ok(hipFree(dz), "free");
+  }
+  // whole-array statistics (float64 accumulation)
+  float* d4 = nullptr;
+  hip_ok(hipMalloc(&d4, 16), "hipMalloc");
+  CHECK(pdd_global_stats(dcm, C, N, N, d4, nullptr) == 0, "global_stats: %s", pdd_last_error());
+  std::vector<float> st = host_copy(d4, 4);
+  double s1 = 0, s2 = 0, mn = 1e30, mx = -1e30;
+  for (float v : cm) {
+    s1 += v;
+    mn = std::min(mn, (double)v);
+    mx = std::max(mx, (double)v);
+  }
+  const double mean = s1 / (double)cm.size();
+  for (float v : cm) s2 += (v - mean) * (v - mean);
+  const double sd = std::sqrt(s2 / (double)cm.size());
+  CHECK(std::fabs(st[0] - mean) <= 1e-4 * std::max(1.0, std::fabs(mean)) &&
+            std::fabs(st[1] - sd) <= 1e-4 * std::max(1.0, sd) && st[2] == mn && st[3] == mx,
+        "global_stats C=%lld N=%lld: {%g %g %g %g} want {%g %g %g %g}", (long long)C,
+        (long long)N, st[0], st[1], st[2], st[3], mean, sd, mn, mx);
+  hip_ok(hipFree(d4), "free");
+  hip_ok(hipFree(dbins), "free");
+  hip_ok(hipFree(dpads), "free");
+  hip_ok(hipFree(dcm), "free");
+  hip_ok(hipFree(dx8), "free");
+}
+
 int main() {
   int ndev = 0;
   hip_ok(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
@@ -153,6 +267,15 @@ int main() {
             ++cases;
           }
 
+  // single-DM ops interleaved with more sweeps (shared per-stream scratch)
+  int ops = 0;
+  for (int64_t C : {16, 64, 2048})
+    for (int64_t N : {300, 4099}) {
+      ops_case(rng, C, N);
+      sweep_case(rng, 64, 3000, 40, 40, (ops & 1) ? PDD_U8 : PDD_F32, false);
+      ++ops;
+    }
+
   // grouped plans: create / info / destroy
   for (int rep = 0; rep < 20; ++rep) {
     const int64_t G = 1 + rep % 4, D = 3 + rep, C = 8 + 8 * (rep % 3);
@@ -163,6 +286,6 @@ int main() {
     CHECK(rc == 0 && q, "grouped create rep %d: %s", rep, pdd_last_error());
     if (q) CHECK(pdd_sweep_plan_destroy(q) == 0, "grouped destroy");
   }
-  std::printf("abi_asan: %d sweep cases, %d failures\n", cases, failures);
+  std::printf("abi_asan: %d sweep cases, %d op cases, %d failures\n", cases, ops, failures);
   return failures ? 1 : 0;
 }

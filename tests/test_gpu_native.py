@@ -1,7 +1,9 @@
 """The C-ABI driver (tests/native/abi_asan.cpp, built by __graft_entry__.build()
 against pypulsar_amd/libpdd.so): argument checks, random sweep grids through
-every tiling rung checked against a host sum, grouped plans and timing pools,
-called straight through include/pdd.h with no Python in between.  It is the
+every tiling rung checked against a host sum, single-DM ops (corner turn,
+shift + group sum with the sliced-partials path, exact integer zero-DM +
+downsample, global statistics) against host loops, grouped plans and timing
+pools, called straight through include/pdd.h with no Python in between.  It is the
 regression test for library scratch reuse across calls: with stream-ordered
 hipMallocAsync/hipFreeAsync images, a sequence of plan/execute/free calls
 produced wrong planes (pool pages released at device synchronisation aliased
