@@ -1086,322 +1086,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
 // window per add against 0.083 for the 48-trial u16 tiles, and the LDS-DMA
 // staging path (~80-130 CU-cycles per KiB) is what binds both kernels.
 #ifdef PDD_SWEEP_DEV
-// For 8-bit input the channel sum runs on the matrix cores (gfx950 i8 MFMA),
-// not on the VALU.  Per DM trial and 16 output times, one
-//     v_mfma_i32_16x16x64_i8  C[m][n] += sum_k A[m][k] * B[k][n]
-// sums 64 channels (K) for 16 times (M): 1024 adds per 16-cycle instruction,
-// twice the VALU add rate, and its operand costs 1 LDS byte per add (the u16
-// VALU path reads 2).
-//   A[m][k] = X'(k, t + m + r_k - phi_k)  gathered by two ds_read_b64_tr_b8:
-//     each 16-lane group reads 8 channel rows x 16 times, lane 2q+p supplying
-//     the 8-byte-aligned address of row q, columns 8p..8p+7 (measured on
-//     gfx950, scripts/probes/tr8_mfma_probe.hip); a row starts at the trial's
-//     shift rounded DOWN to 8, r_k - phi_k, phi_k = r_k mod 8;
-//   B[k][n] = [phi_k == n] routes each channel to the column of its phase, so
-//     C[m][n] holds partial sums for output time t + m - n (n < 8);
-//   X' = x ^ 0x80 = x - 128 as int8 (the pre-pass k_prep8), so the sum is
-//     exact in int32 and the output is sum + 128 * C.
-// A tile = 16 trials (8 waves x 2) x 256 output times; per trial and chunk
-// of 64 channels a wave issues 17 MFMAs (16 subtiles + the spill of the last
-// one into the next 16 times); after the channel loop the phase columns are
-// combined (out[t] = sum_n C[t + n][n]) through LDS.
-// LDS image of a chunk: 4 groups of 16 channels; group row r = bytes
-// [16r, 16r + 16) of each of its 16 channel windows side by side (256 B),
-// so the 32 rows a tr_b8 half-wave reads lie in 16 distinct 16-byte bank
-// columns -- conflict-free for any shifts.  The windows arrive by 1 KiB LDS-DMA
-// (global_load_lds_dwordx4), 4 rows per instruction, issued by all waves
-// NBUF-1 chunks ahead; one s_barrier per chunk.
-constexpr int kMxCh = 64;     // channels per chunk (MFMA K)
-constexpr int kMxRec = 192;   // metadata bytes per (trial, chunk): 64 phases + 32 offset pairs
-
-// i8 image in the kernel's LDS layout, so every staging DMA reads 1 KiB of
-// contiguous global memory:  R8g[grp][row][c16][16 B] holds the samples
-// X(16 grp + c16, base + 16 row + i) ^ 0x80, i < 16 (x - 128 as int8), with the
-// reference pads (value / rotate) outside [0, N); channels >= C are 0 (they
-// contribute 0).  One thread writes 4 rows of one channel (64 input bytes).
-__global__ __launch_bounds__(256) void k_prep8(const uint8_t* __restrict__ x, int64_t ld, int64_t N,
-                                               int C, int64_t base, int64_t nrows, int pad_mode,
-                                               const float* __restrict__ padvals,
-                                               uint8_t* __restrict__ R8g, int fast) {
-  const int grp = blockIdx.y;
-  const int c16 = threadIdx.x & 15;
-  const int c = grp * 16 + c16;
-  const int64_t row0 = ((int64_t)blockIdx.x * 16 + (threadIdx.x >> 4)) * 4;
-  uint8_t* dst = R8g + ((int64_t)grp * nrows) * 256 + c16 * 16;
-  uint4 o[4];
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const int64_t row = row0 + rr;
-    if (row >= nrows) break;
-    if (c >= C) {
-      o[rr] = make_uint4(0u, 0u, 0u, 0u);
-      continue;
-    }
-    const uint8_t* xr = x + (int64_t)c * ld;
-    const int64_t s0 = base + 16 * row;
-    if (fast && s0 >= 0 && s0 + 16 <= N) {
-      const uint4 v = *reinterpret_cast<const uint4*>(xr + s0);
-      o[rr] = make_uint4(v.x ^ 0x80808080u, v.y ^ 0x80808080u, v.z ^ 0x80808080u, v.w ^ 0x80808080u);
-    } else {
-      const uint32_t pv = (pad_mode == PDD_PAD_VALUE) ? (uint32_t)padvals[c] : 0u;
-      uint32_t wv[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        uint32_t acc = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int64_t s = s0 + 4 * q + i;
-          uint32_t v;
-          if (s >= 0 && s < N) v = xr[s];
-          else if (pad_mode == PDD_PAD_ROTATE) v = xr[wrap_mod(s, N)];
-          else v = pv;
-          acc |= ((v ^ 0x80u) & 0xffu) << (8 * i);
-        }
-        wv[q] = acc;
-      }
-      o[rr] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-    }
-  }
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr)
-    if (row0 + rr < nrows) *reinterpret_cast<uint4*>(dst + (row0 + rr) * 256) = o[rr];
-}
-
-// one 1 KiB LDS-DMA wave-instruction: lane l copies 16 B from src (its own
-// address) to LDS byte lds_dst + 16 l (lds_dst wave-uniform)
-__device__ __forceinline__ void dma16(uint32_t lds_dst, const void* src) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_dst))
-      : "memory");
-}
-
-typedef int i32x4_mx __attribute__((ext_vector_type(4)));
-typedef i32x4_mx i32x4_mx_acc;
-typedef int i32x2_mx __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) i32x2_mx lds_i32x2_mx;
-typedef __attribute__((address_space(3))) i32x4_mx lds_i32x4_mx;
-typedef __attribute__((address_space(3))) int lds_int_mx;
-typedef __attribute__((address_space(3))) uint16_t lds_u16_mx;
-typedef __attribute__((address_space(3))) uint8_t lds_u8_mx;
-
-__host__ __device__ constexpr int mx_scr_bytes(int S) { return (16 * (S + 1) + 32) * 32; }
-
-// ds_read_b64_tr_b8 through asm: the compiler neither waits for it nor folds a
-// prefetch ring back into one register set; the caller waits with mx_wait.
-template <int OFF>
-__device__ __forceinline__ void mx_tr8(i32x2_mx& r, uint32_t addr) {
-  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF) : "memory");
-}
-// s_waitcnt lgkmcnt(N) tied to the two operand halves it releases
-template <int N>
-__device__ __forceinline__ void mx_wait(i32x2_mx& a, i32x2_mx& b) {
-  static_assert(N >= 0 && N <= 15, "lgkmcnt field");
-  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
-}
-
-// One step of the MFMA sequence (I = trial * (S + 1) + subtile): wait for
-// its operands, issue the MFMA, refill the ring PF steps ahead.  Expanded by
-// a fold over an integer sequence so every index is a compile-time constant.
-template <int S, int DPW, int PF>
-struct MxSeq {
-  static constexpr int NM = DPW * (S + 1), NSL = PF + 1;
-  template <int I>
-  static __device__ __forceinline__ void read(i32x2_mx* r0, i32x2_mx* r1, const uint32_t* a0,
-                                              const uint32_t* a1) {
-    mx_tr8<256 * (I % (S + 1))>(r0[I % NSL], a0[I / (S + 1)]);
-    mx_tr8<256 * (I % (S + 1))>(r1[I % NSL], a1[I / (S + 1)]);
-  }
-  template <int I>
-  static __device__ __forceinline__ void step(i32x2_mx* r0, i32x2_mx* r1, i32x4_mx_acc* acc,
-                                              const i32x4_mx_acc* B, const uint32_t* a0,
-                                              const uint32_t* a1) {
-    constexpr int ahead = (NM - 1 - I) < (PF - 1) ? (NM - 1 - I) : (PF - 1);
-    mx_wait<2 * ahead>(r0[I % NSL], r1[I % NSL]);
-    const i32x4_mx_acc A = (i32x4_mx_acc){r0[I % NSL].x, r0[I % NSL].y, r1[I % NSL].x, r1[I % NSL].y};
-    acc[I] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B[I / (S + 1)], acc[I], 0, 0, 0);
-    if constexpr (I + PF < NM) read<I + PF>(r0, r1, a0, a1);
-  }
-  template <int... Is>
-  static __device__ __forceinline__ void prologue(std::integer_sequence<int, Is...>, i32x2_mx* r0,
-                                                  i32x2_mx* r1, const uint32_t* a0,
-                                                  const uint32_t* a1) {
-    (read<Is>(r0, r1, a0, a1), ...);
-  }
-  template <int... Is>
-  static __device__ __forceinline__ void run(std::integer_sequence<int, Is...>, i32x2_mx* r0,
-                                             i32x2_mx* r1, i32x4_mx_acc* acc, const i32x4_mx_acc* B,
-                                             const uint32_t* a0, const uint32_t* a1) {
-    (step<Is>(r0, r1, acc, B, a0, a1), ...);
-  }
-};
-
-template <int NW, int DPW, int S, int NBUF>
-__global__ __launch_bounds__(NW * 64) void k_sweep_mx(
-    const uint8_t* __restrict__ R8, int64_t nR8, int nchunk, const uint8_t* __restrict__ meta,  // nR8: rows per group
-    const uint16_t* __restrict__ win, const uint8_t* __restrict__ rows, int rows_max,
-    float* __restrict__ out, int64_t ld_out, int D, int64_t t_base, int64_t t_end, int n_dblk,
-    int corr, int dbg) {
-  constexpr int DB = NW * DPW;
-  constexpr int TT = 16 * S;
-  constexpr int META_B = DB * kMxRec;
-  static_assert(META_B % 1024 == 0, "metadata must be whole 1 KiB DMA pieces");
-  extern __shared__ __attribute__((aligned(16))) uint8_t smx[];
-  const int ngrp = nchunk * 4;            // 16-channel groups
-  const int WIN_B = (2 * ngrp + 15) & ~15;
-  const int ROWS_B = (4 * nchunk + 15) & ~15;
-  const int GB = rows_max * 256;         // bytes per 16-channel group
-  const int BUF = 4 * GB + META_B;       // bytes per chunk buffer
-  const uint32_t lds0 = lds_addr_of(smx);
-  const uint32_t buf0 = lds0 + WIN_B + ROWS_B;
-
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  // XCD-aware tile order: blocks b and b + 8 share an XCD; XCD x owns the
-  // trial blocks [x R, (x + 1) R) (R = n_dblk rounded up to 8, / 8) and walks
-  // them trial block fastest, so its ~32 resident tiles are CONSECUTIVE trial
-  // blocks of one time tile, whose channel windows overlap (adjacent trial
-  // blocks' shifts differ by about one span): the staging is served from the
-  // XCD's L2 instead of the Infinity Cache.
-  const int R = (n_dblk + 7) / 8;
-  const int xcd = blockIdx.x % 8, kx = blockIdx.x / 8;
-  const int dblk = xcd * R + kx % R;
-  if (dblk >= n_dblk) return;  // padding of the trial-block ranges
-  const int64_t t0 = (int64_t)(kx / R) * TT;
-
-  // per-block tables: window start of every 16-channel group (u16, in
-  // samples, a multiple of 16) and staged rows per group
-  {
-    const uint16_t* wsrc = win + (int64_t)dblk * ngrp;
-    uint16_t* wdst = reinterpret_cast<uint16_t*>(smx);
-    for (int i = threadIdx.x; i < ngrp; i += NW * 64) wdst[i] = wsrc[i];
-    const uint32_t* rsrc = reinterpret_cast<const uint32_t*>(rows + (int64_t)dblk * nchunk * 4);
-    uint32_t* rdst = reinterpret_cast<uint32_t*>(smx + WIN_B);
-    for (int i = threadIdx.x; i < nchunk; i += NW * 64) rdst[i] = rsrc[i];
-  }
-  __syncthreads();
-
-  const uint8_t* meta_b = meta + (int64_t)dblk * nchunk * META_B;
-  auto issue = [&](int k) -> int {
-    if (dbg & 1) return 0;  // dev: no staging (timing only, wrong results)
-    const uint32_t bufb = buf0 + (uint32_t)((k % NBUF) * BUF);
-    int n = 0, pi = 0;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int grp = k * 4 + g;
-      const int rg = __builtin_amdgcn_readfirstlane(*(const lds_u8_mx*)(uintptr_t)(lds0 + WIN_B + grp));
-      const int ws = __builtin_amdgcn_readfirstlane(*(const lds_u16_mx*)(uintptr_t)(lds0 + 2 * grp));
-      // 4 rows (1 KiB, contiguous) per piece
-      const uint8_t* src = R8 + ((int64_t)grp * nR8 + (t0 + ws) / 16) * 256 + 16 * lane;
-      for (int pg = 0; pg < (rg >> 2); ++pg, ++pi)
-        if (pi % NW == w) {
-          dma16(bufb + (uint32_t)(g * GB + pg * 1024), src + 1024 * pg);
-          ++n;
-        }
-    }
-#pragma unroll
-    for (int m = 0; m < META_B / 1024; ++m, ++pi)
-      if (pi % NW == w) {
-        dma16(bufb + (uint32_t)(4 * GB + m * 1024), meta_b + (int64_t)k * META_B + m * 1024 + 16 * lane);
-        ++n;
-      }
-    return n;
-  };
-
-  i32x4_mx acc[DPW][S + 1];
-#pragma unroll
-  for (int j = 0; j < DPW; ++j)
-#pragma unroll
-    for (int s2 = 0; s2 <= S; ++s2) acc[j][s2] = (i32x4_mx){0, 0, 0, 0};
-
-  int hist[NBUF];
-#pragma unroll
-  for (int i = 0; i < NBUF; ++i) hist[i] = 0;
-#pragma unroll
-  for (int s2 = 0; s2 < NBUF - 1; ++s2) {
-#pragma unroll
-    for (int i = NBUF - 1; i > 0; --i) hist[i] = hist[i - 1];
-    hist[0] = s2 < nchunk ? issue(s2) : 0;
-  }
-  const int g4 = lane >> 4;               // 16-lane group
-  const int qq = (lane & 15) >> 1, pp = lane & 1;
-  const uint32_t nn = (uint32_t)(lane & 15) * 0x01010101u;
-  for (int k = 0; k < nchunk; ++k) {
-    int younger = 0;
-#pragma unroll
-    for (int i = 0; i < NBUF - 2; ++i) younger += hist[i];
-    wait_vmcnt(younger);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    {
-      const int n = (k + NBUF - 1 < nchunk) ? issue(k + NBUF - 1) : 0;
-#pragma unroll
-      for (int i = NBUF - 1; i > 0; --i) hist[i] = hist[i - 1];
-      hist[0] = n;
-    }
-    if (dbg & 2) continue;  // dev: no compute (timing only, wrong results)
-    const uint32_t bufb = buf0 + (uint32_t)((k % NBUF) * BUF);
-    // per trial: B (phase one-hot) and the two row addresses of this lane
-    i32x4_mx B[DPW];
-    uint32_t a0[DPW], a1[DPW];
-#pragma unroll
-    for (int j = 0; j < DPW; ++j) {
-      const uint32_t mrec = bufb + (uint32_t)(4 * GB + (w * DPW + j) * kMxRec);
-      const i32x4_mx ph = *(const lds_i32x4_mx*)(uintptr_t)(mrec + 16 * g4);
-      const uint32_t offp = (uint32_t)*(const lds_int_mx*)(uintptr_t)(mrec + 64 + 4 * (8 * g4 + qq));
-      // B[k][n] = [phase_k == n]: bytes of ph ^ n that are zero -> 1
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        B[j][e] = (int)(((~(((uint32_t)ph[e] ^ nn) + 0x7F7F7F7Fu)) >> 7) & 0x01010101u);
-      const uint32_t o0 = (offp & 0xffffu) + 8u * pp, o1 = (offp >> 16) + 8u * pp;
-      const uint32_t col = (uint32_t)((8 * (g4 & 1) + qq) * 16);
-      a0[j] = bufb + (uint32_t)((g4 >> 1) * GB) + (o0 >> 4) * 256u + col + (o0 & 15u);
-      a1[j] = bufb + (uint32_t)((2 + (g4 >> 1)) * GB) + (o1 >> 4) * 256u + col + (o1 & 15u);
-    }
-    // DPW x (S+1) MFMAs in one sequence; the two tr_b8 reads of MFMA i are
-    // issued PF MFMAs ahead into a ring of PF + 1 operand slots (a refill never
-    // targets the slot the current MFMA reads); before MFMA i the wave waits
-    // for all but the younger reads still in flight (LDS reads retire in order)
-    using Seq = MxSeq<S, DPW, 6>;
-    i32x2_mx r0[Seq::NSL], r1[Seq::NSL];
-    Seq::prologue(std::make_integer_sequence<int, 6>{}, r0, r1, a0, a1);
-    Seq::run(std::make_integer_sequence<int, Seq::NM>{}, r0, r1, &acc[0][0], B, a0, a1);
-  }
-  // ---- combine the phase columns: out[t] = sum_n C[t + n][n] + 128 C
-  __syncthreads();
-  const uint32_t sb = buf0 + (uint32_t)(w * mx_scr_bytes(S));
-  const int n = lane & 15;
-#pragma unroll
-  for (int j = 0; j < DPW; ++j) {
-    const int d = dblk * DB + w * DPW + j;
-    if (n < 8) {
-#pragma unroll
-      for (int s2 = 0; s2 <= S; ++s2)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int rho = 16 * s2 + 4 * g4 + i - n + 8;
-          *(lds_int_mx*)(uintptr_t)(sb + (uint32_t)((rho * 8 + n) * 4)) = acc[j][s2][i];
-        }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int u = 0; u < TT / 64; ++u) {
-      const int r = lane + 64 * u;
-      const i32x4_mx x0 = *(const lds_i32x4_mx*)(uintptr_t)(sb + (uint32_t)((r + 8) * 32));
-      const i32x4_mx x1 = *(const lds_i32x4_mx*)(uintptr_t)(sb + (uint32_t)((r + 8) * 32 + 16));
-      const int sum = x0.x + x0.y + x0.z + x0.w + x1.x + x1.y + x1.z + x1.w + corr;
-      const int64_t t = t_base + t0 + r;
-      if (d < D && t < t_end) out[(int64_t)d * ld_out + t] = (float)sum;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
-}
+#include "dev/sweep_mx_kernel.inc"
 #endif  // PDD_SWEEP_DEV
 
 // ------------------------------------------------------------------ variants
@@ -1566,172 +1251,12 @@ struct pdd_sweep_plan {
 using namespace pdd;
 
 #ifdef PDD_SWEEP_DEV
-// Host: tables of the 8-bit MFMA sweep (kind 2) for a [D][C] table; 1 = the
-// variant does not fit this grid (caller tries the next one), < 0 = error.
-static int mx_plan_create(const int32_t* htab, int64_t D, int64_t C, const Variant& v, int vi,
-                          pdd_sweep_plan** plan_out) {
-  const int DB = v.DB(), S = v.S;
-  const int64_t n_dblk = cdiv(D, DB), Dpad = n_dblk * DB;
-  const int64_t nchunk = cdiv(C, kMxCh), Cpad = nchunk * kMxCh;
-  int mn = INT32_MAX, mx = INT32_MIN;
-  for (int64_t i = 0; i < D * C; ++i) {
-    mn = std::min(mn, (int)htab[i]);
-    mx = std::max(mx, (int)htab[i]);
-  }
-  const int64_t lo = std::min(0, mn), hi = std::max(0, mx);
-  if (hi - lo + 16 * S + 256 >= 65536) return 1;  // window starts are u16
-  const int64_t WIN_B = (2 * (Cpad / 16) + 15) & ~15, ROWS_B = (4 * nchunk + 15) & ~15;
-  const int64_t META_B = (int64_t)DB * kMxRec;
-  const int64_t ngrp = Cpad / 16;
-  std::vector<uint16_t> win((size_t)(n_dblk * ngrp), 0);
-  std::vector<uint8_t> rows((size_t)(n_dblk * nchunk * 4), 0);
-  std::vector<uint8_t> meta((size_t)(n_dblk * nchunk * META_B), 0);
-  std::vector<int> offk((size_t)Cpad), phk((size_t)Cpad);
-  int rows_max = 0;
-  for (int64_t b = 0; b < n_dblk; ++b) {
-    // window start of every 16-channel group: the smallest shift of the
-    // block over its channels, 16-aligned (one staging window per group)
-    for (int64_t gi = 0; gi < ngrp; ++gi) {
-      int bmin = INT32_MAX;
-      for (int64_t c = gi * 16; c < std::min(C, gi * 16 + 16); ++c)
-        for (int64_t d = b * DB; d < (b + 1) * DB; ++d)
-          bmin = std::min(bmin, (int)htab[std::min(d, D - 1) * C + c]);
-      win[(size_t)(b * ngrp + gi)] = bmin == INT32_MAX ? 0 : (uint16_t)((bmin - lo) & ~15);
-    }
-    for (int64_t k = 0; k < nchunk; ++k) {
-      int rmax[4] = {0, 0, 0, 0};
-      for (int i = 0; i < DB; ++i) {
-        const int64_t d = std::min(b * DB + i, D - 1);
-        for (int ch = 0; ch < kMxCh; ++ch) {
-          const int64_t c = k * kMxCh + ch;
-          int off = 0, ph = 0;
-          if (c < C) {
-            const int64_t r = (int64_t)htab[d * C + c] - lo;
-            off = (int)((r & ~7) - win[(size_t)(b * ngrp + c / 16)]);
-            ph = (int)(r & 7);
-          }
-          offk[(size_t)ch] = off;
-          phk[(size_t)ch] = ph;
-          rmax[ch >> 4] = std::max(rmax[ch >> 4], off);
-        }
-        uint8_t* rec = meta.data() + (size_t)(((b * nchunk + k) * DB + i) * kMxRec);
-        for (int g = 0; g < 4; ++g)
-          for (int j = 0; j < 16; ++j) rec[16 * g + j] = (uint8_t)phk[(size_t)(32 * (j >> 3) + 8 * g + (j & 7))];
-        for (int g = 0; g < 4; ++g)
-          for (int q = 0; q < 8; ++q) {
-            const uint32_t o = (uint32_t)offk[(size_t)(8 * g + q)] |
-                               ((uint32_t)offk[(size_t)(32 + 8 * g + q)] << 16);
-            std::memcpy(rec + 64 + 4 * (8 * g + q), &o, 4);
-          }
-      }
-      for (int g = 0; g < 4; ++g) {
-        // last byte a subtile read touches: 16 S + off + 15
-        const int need = (16 * S + rmax[g] + 15) / 16 + 1;
-        const int rg = (need + 3) & ~3;
-        if (rg > 255) return 1;
-        rows[(size_t)((b * nchunk + k) * 4 + g)] = (uint8_t)rg;
-        rows_max = std::max(rows_max, rg);
-      }
-    }
-  }
-  const int64_t BUF = 4 * (int64_t)rows_max * 256 + META_B;
-  const int64_t need = WIN_B + ROWS_B + std::max<int64_t>(v.NBUF * BUF, v.NW * mx_scr_bytes(S));
-  if (need > kLdsMax) return 1;
-  sweep_mx_fn kf = mx_kernel_for(v);
-  PDD_REQUIRE(kf != nullptr, "pdd_sweep_plan_create: no MFMA kernel for variant %d", vi);
-  pdd_sweep_plan* p = new pdd_sweep_plan();
-  p->v = v;
-  p->D = D;
-  p->C = C;
-  p->Dpad = Dpad;
-  p->n_dblk = n_dblk;
-  p->max_span = (int)(hi - lo);
-  p->stride = 0;
-  p->cc = kMxCh;
-  p->lds_bytes = (int)need;
-  p->vi = vi;
-  p->dtype = PDD_U8;
-  p->n_grp = 1;
-  p->max_bin = mx;
-  p->min_bin = mn;
-  p->rows_max = rows_max;
-  p->nchunk = (int)nchunk;
-  hipError_t e = hipMalloc(&p->d_meta, meta.size());
-  if (e == hipSuccess) e = hipMalloc(&p->d_win, win.size() * sizeof(uint16_t));
-  if (e == hipSuccess) e = hipMalloc(&p->d_rows, rows.size());
-  if (e == hipSuccess) e = hipMemcpy(p->d_meta, meta.data(), meta.size(), hipMemcpyHostToDevice);
-  if (e == hipSuccess)
-    e = hipMemcpy(p->d_win, win.data(), win.size() * sizeof(uint16_t), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(p->d_rows, rows.data(), rows.size(), hipMemcpyHostToDevice);
-  if (e == hipSuccess && need > 64 * 1024)
-    e = hipFuncSetAttribute((const void*)kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need);
-  if (e != hipSuccess) {
-    set_error("pdd_sweep_plan_create: %s", hipGetErrorString(e));
-    pdd_sweep_plan_destroy(p);
-    return -2;
-  }
-  *plan_out = p;
-  return 0;
-}
-
-// 8-bit MFMA path: time segments whose i8 image R8 ([Cpad/16][rows][16][16] bytes) fits
-// the scratch budget; each segment is one k_prep8 + one k_sweep_mx.
-static int execute_mx(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t ld, int pad_mode,
-                      const float* padvals, float* out, int64_t ld_out, int64_t n_out,
-                      void* stream) {
-  const int S = p->v.S, TT = 16 * S;
-  const int64_t C = p->C, Cpad = (int64_t)p->nchunk * kMxCh;
-  const int64_t lo = std::min(0, p->min_bin), hi = std::max(0, p->max_bin);
-  const int64_t extra = (hi - lo) + 16 * S + 128;
-  int64_t budget = (int64_t)8 << 30;
-  if (const char* e = getenv("PDD_SWEEP_SEG_BYTES")) budget = std::max<int64_t>(atoll(e), 1 << 16);
-  int64_t seg = (budget / Cpad - extra) / TT * TT;
-  PDD_REQUIRE(seg > 0, "pdd_sweep_execute: delay span %lld too wide for the segment budget",
-              (long long)(hi - lo));
-  const int64_t nseg = cdiv(n_out, seg);
-  seg = cdiv(cdiv(n_out, nseg), TT) * TT;  // equal segments of whole tiles
-  const int64_t nR8_alloc = (seg + extra + 15) / 16 * 16;
-  uint8_t* R8 = nullptr;
-  hipStream_t st = as_stream(stream);
-  R8 = static_cast<uint8_t*>(scratch(st, kScratchImage, (size_t)(Cpad * nR8_alloc)));
-  if (!R8) return -2;
-  sweep_mx_fn kf = mx_kernel_for(p->v);
-  int rc = kf ? 0 : -1;
-  for (int64_t t_base = 0; t_base < n_out && rc == 0; t_base += seg) {
-    const int64_t cnt = std::min(seg, n_out - t_base);
-    const int64_t n_tblk = cdiv(cnt, TT);
-    const int64_t nrows = cdiv(n_tblk * TT + extra, 16);  // 16-sample rows per group
-    const int64_t base = t_base + lo;
-    const int fast = ((uintptr_t)x % 16 == 0) && (ld % 16 == 0) && (base % 16 == 0);
-    hipLaunchKernelGGL(k_prep8, dim3((unsigned)cdiv(nrows, 64), (unsigned)(Cpad / 16)), dim3(256),
-                       0, st, (const uint8_t*)x, ld, N, (int)C, base, nrows, pad_mode, padvals, R8,
-                       fast);
-    if (hipGetLastError() != hipSuccess) { rc = -3; break; }
-    const int64_t blocks = n_tblk * cdiv(p->n_dblk, 8) * 8;  // see k_sweep_mx tile order
-    if (blocks >= (1ll << 31)) { rc = -1; break; }
-    pdd_sweep_plan* pm = const_cast<pdd_sweep_plan*>(p);
-    const bool bracket = p->timing && p->timed < pdd_sweep_plan::kEvPairs;
-    if (p->timing && !bracket) pm->dropped++;
-    if (bracket) (void)hipEventRecord(p->ev[2 * p->timed], st);
-    hipLaunchKernelGGL(kf, dim3((unsigned)blocks), dim3(p->v.NW * 64), p->lds_bytes, st, R8, nrows,
-                       p->nchunk, p->d_meta, p->d_win, p->d_rows, p->rows_max, out, ld_out,
-                       (int)p->D, t_base, t_base + cnt, (int)p->n_dblk, (int)(128 * C),
-                       debug_flags());
-    if (hipGetLastError() != hipSuccess) rc = -3;
-    if (bracket) {
-      (void)hipEventRecord(p->ev[2 * p->timed + 1], st);
-      pm->timed++;
-    }
-  }
-  if (rc == -1) set_error("pdd_sweep_execute: grid too large or no MFMA kernel");
-  if (rc == -3) set_error("pdd_sweep_execute: kernel launch failed");
-  return rc;
-}
+#include "dev/sweep_mx_host.inc"
 #endif  // PDD_SWEEP_DEV
 
 // Interleaved path: the output is produced in time segments whose
-// interleaved copy R fits a scratch budget (stream-ordered allocation, freed
-// after the segment loop); each segment is one k_interleave + one k_sweep_il.
+// interleaved copy R fits a scratch budget (the library's per-stream
+// scratch, pdd::scratch, reused across calls); each segment is one k_interleave + one k_sweep_il.
 // IlExtra.ds > 1: x is the 8-bit block at the raw rate (channel-major rows
 // of N * ds samples, lay.ld apart), co-added by ds in the interleave
 // pre-pass.  IlExtra.r2_pad: the output is the next sweep's quarters image
