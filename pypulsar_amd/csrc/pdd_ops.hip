@@ -785,6 +785,9 @@ __device__ __forceinline__ float smooth_src(const float* row, int64_t j, int64_t
 
 constexpr int kSmoothOpt = 16;                 // outputs per thread
 constexpr int kSmoothTile = 256 * kSmoothOpt;  // outputs per workgroup
+// LDS slot of window sample j: one pad float after every 16, so the lanes'
+// sliding reads (16 samples apart) fall in distinct banks (was 8-way)
+__device__ __forceinline__ int64_t smooth_slot(int64_t j) { return j + (j >> 4); }
 __global__ __launch_bounds__(256) void k_smooth(const float* __restrict__ x, int64_t N, int64_t ld,
                                                 int64_t w, int pad_mode,
                                                 const float* __restrict__ padvals,
@@ -804,10 +807,10 @@ __global__ __launch_bounds__(256) void k_smooth(const float* __restrict__ x, int
     for (int q = 0; q < kSmoothOpt; ++q)
       v[q] = smooth_src(row, j0 + q * 256 + threadIdx.x, N, pad_mode, pad);
 #pragma unroll
-    for (int q = 0; q < kSmoothOpt; ++q) win[q * 256 + threadIdx.x] = v[q];
+    for (int q = 0; q < kSmoothOpt; ++q) win[smooth_slot(q * 256 + threadIdx.x)] = v[q];
     for (int64_t i = kSmoothTile + threadIdx.x; i < nw; i += 256)
-      win[i] = smooth_src(row, j0 + i, N, pad_mode, pad);
-    if (threadIdx.x == 0) win[nw] = 0.f;  // the spare slot the sliding window reads last
+      win[smooth_slot(i)] = smooth_src(row, j0 + i, N, pad_mode, pad);
+    if (threadIdx.x == 0) win[smooth_slot(nw)] = 0.f;  // the spare slot the sliding window reads last
   }
   __syncthreads();
   const double k = 1.0 / sqrt((double)w);
@@ -819,7 +822,7 @@ __global__ __launch_bounds__(256) void k_smooth(const float* __restrict__ x, int
   double sm[kSmoothOpt];
 #pragma unroll
   for (int q = 0; q < kSmoothOpt; ++q) {
-    r[q] = win[o + q];
+    r[q] = win[smooth_slot(o + q)];
     sm[q] = 0.0;
   }
   for (int64_t i = 0; i < w; ++i) {
@@ -827,20 +830,31 @@ __global__ __launch_bounds__(256) void k_smooth(const float* __restrict__ x, int
     for (int q = 0; q < kSmoothOpt; ++q) sm[q] += (double)r[q];
 #pragma unroll
     for (int q = 0; q < kSmoothOpt - 1; ++q) r[q] = r[q + 1];
-    r[kSmoothOpt - 1] = win[o + kSmoothOpt + i];
+    r[kSmoothOpt - 1] = win[smooth_slot(o + kSmoothOpt + i)];
   }
-  const int64_t t = t0 + o;
+  // results through the LDS window (free after the barrier) so every store
+  // instruction writes 1 KiB of consecutive outputs (a thread's own 16
+  // contiguous outputs would spread each instruction over 4 KiB)
   float* orow = out + c * ld_out;
-  if (t + kSmoothOpt <= N && (((uintptr_t)(orow + t)) & 15) == 0) {
+  __syncthreads();
 #pragma unroll
-    for (int q = 0; q < kSmoothOpt; q += 4)
-      *reinterpret_cast<float4*>(orow + t + q) =
-          make_float4((float)(sm[q] * k), (float)(sm[q + 1] * k), (float)(sm[q + 2] * k),
-                      (float)(sm[q + 3] * k));
-  } else {
+  for (int q = 0; q < kSmoothOpt; ++q) win[smooth_slot(o + q)] = (float)(sm[q] * k);
+  __syncthreads();
+  const bool vec = (((uintptr_t)(orow + t0)) & 15) == 0;
 #pragma unroll
-    for (int q = 0; q < kSmoothOpt; ++q)
-      if (t + q < N) orow[t + q] = (float)(sm[q] * k);
+  for (int q = 0; q < kSmoothOpt / 4; ++q) {
+    const int i0 = q * 1024 + 4 * threadIdx.x;
+    const int64_t t = t0 + i0;
+    const float a = win[smooth_slot(i0)], b = win[smooth_slot(i0 + 1)],
+                d = win[smooth_slot(i0 + 2)], e = win[smooth_slot(i0 + 3)];
+    if (vec && t + 4 <= N) {
+      *reinterpret_cast<float4*>(orow + t) = make_float4(a, b, d, e);
+    } else {
+      if (t < N) orow[t] = a;
+      if (t + 1 < N) orow[t + 1] = b;
+      if (t + 2 < N) orow[t + 2] = d;
+      if (t + 3 < N) orow[t + 3] = e;
+    }
   }
 }
 
@@ -1369,7 +1383,8 @@ int pdd_smooth(const float* x, int64_t C, int64_t N, int64_t ld, int64_t width, 
   if (C == 0) return 0;
   const int64_t tiles = cdiv(N, kSmoothTile);
   PDD_REQUIRE(C * tiles < (1ll << 31), "pdd_smooth: too large");
-  const size_t lds = (size_t)(kSmoothTile + width) * sizeof(float);  // <= 48 KiB
+  const int64_t nslot = kSmoothTile + width;  // window + the spare sample
+  const size_t lds = (size_t)(nslot + nslot / 16 + 1) * sizeof(float);  // <= 48 KiB
   k_smooth<<<(unsigned)(C * tiles), 256, lds, as_stream(stream)>>>(x, N, ld, width, pad_mode,
                                                                    padvals, out, ld_out, tiles);
   PDD_LAUNCHED();
