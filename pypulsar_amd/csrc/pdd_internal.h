@@ -42,7 +42,7 @@ void set_error(const char* fmt, ...);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
-// Device scratch owned by the library, one buffer per (stream, slot), grown
+// Device scratch owned by the library, one buffer per (device, stream, slot), grown
 // with hipMalloc and kept for reuse.  Work on one stream is ordered, so
 // consecutive calls on the same stream share a slot safely; a call that
 // needs two buffers at once uses two slots.  (Replaces stream-ordered

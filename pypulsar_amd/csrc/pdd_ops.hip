@@ -26,6 +26,7 @@ void set_error(const char* fmt, ...) {
 
 namespace {
 struct ScratchBuf {
+  int dev;  // the null stream is per device: key by device too
   hipStream_t st;
   int slot;
   void* ptr;
@@ -38,8 +39,13 @@ std::vector<ScratchBuf> g_scratch;
 void* scratch(hipStream_t st, int slot, size_t bytes) {
   std::lock_guard<std::mutex> lock(g_scratch_mu);
   bytes = std::max<size_t>(bytes, 256);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    set_error("device scratch: hipGetDevice failed");
+    return nullptr;
+  }
   for (auto& b : g_scratch) {
-    if (b.st != st || b.slot != slot) continue;
+    if (b.dev != dev || b.st != st || b.slot != slot) continue;
     if (b.bytes >= bytes) return b.ptr;
     // grow: the stream's queued work may still read the old buffer
     hipError_t e = hipStreamSynchronize(st);
@@ -61,7 +67,7 @@ void* scratch(hipStream_t st, int slot, size_t bytes) {
     set_error("device scratch (%zu bytes): %s", bytes, hipGetErrorString(e));
     return nullptr;
   }
-  g_scratch.push_back({st, slot, p, bytes});
+  g_scratch.push_back({dev, st, slot, p, bytes});
   return p;
 }
 
@@ -1060,10 +1066,16 @@ const char* pdd_last_error(void) { return pdd::g_err; }
 
 int pdd_scratch_release(void) {
   std::lock_guard<std::mutex> lock(pdd::g_scratch_mu);
-  PDD_HIP(hipDeviceSynchronize());
-  for (auto& b : pdd::g_scratch)
-    if (b.ptr) (void)hipFree(b.ptr);
+  int cur = 0;
+  PDD_HIP(hipGetDevice(&cur));
+  for (auto& b : pdd::g_scratch) {
+    if (!b.ptr) continue;
+    PDD_HIP(hipSetDevice(b.dev));
+    PDD_HIP(hipDeviceSynchronize());
+    (void)hipFree(b.ptr);
+  }
   pdd::g_scratch.clear();
+  PDD_HIP(hipSetDevice(cur));
   return 0;
 }
 
