@@ -737,6 +737,30 @@ __device__ __forceinline__ void il_tile_of(int bid, int n_tblk, int n_dblk, int 
   tblk = x * TX + band * GT + r / gj;
 }
 
+// Eight consecutive metadata rows' window fields {bmin, span, offset,
+// source row} (row stride ROW ints) by eight scalar loads and one wait
+// (the sweep's loader waves; they read no LDS).  The plan pads the table so
+// eight rows from any chunk start are inside the allocation.
+typedef int i32x4s_t __attribute__((ext_vector_type(4)));
+struct il_rows8 {
+  i32x4s_t r0, r1, r2, r3, r4, r5, r6, r7;
+};
+template <int ROW>
+__device__ __forceinline__ il_rows8 il_load_rows8(const int* p) {
+  il_rows8 o;
+  asm volatile(
+      "s_load_dwordx4 %0, %8, %9\n\ts_load_dwordx4 %1, %8, %10\n\t"
+      "s_load_dwordx4 %2, %8, %11\n\ts_load_dwordx4 %3, %8, %12\n\t"
+      "s_load_dwordx4 %4, %8, %13\n\ts_load_dwordx4 %5, %8, %14\n\t"
+      "s_load_dwordx4 %6, %8, %15\n\ts_load_dwordx4 %7, %8, %16\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=s"(o.r0), "=s"(o.r1), "=s"(o.r2), "=s"(o.r3), "=s"(o.r4), "=s"(o.r5), "=s"(o.r6),
+        "=s"(o.r7)
+      : "s"(p), "i"(0), "i"(ROW * 4), "i"(2 * ROW * 4), "i"(3 * ROW * 4), "i"(4 * ROW * 4),
+        "i"(5 * ROW * 4), "i"(6 * ROW * 4), "i"(7 * ROW * 4));
+  return o;
+}
+
 // a + b + c: one v_add3_u32 (two packed-u16 sample adds per lane)
 __device__ __forceinline__ uint32_t add3_u32(uint32_t a, uint32_t b, uint32_t c) {
   return a + b + c;
@@ -827,19 +851,8 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       static_assert(CC <= 8, "at most eight rows per chunk");
       const int e = cht_t[1 + k];
       const int ncc = e >> 20;
-      const int* mrow = mt_b + (int64_t)(e & 0xfffff) * ROW + DB;
-      typedef int i32x4s_t __attribute__((ext_vector_type(4)));
-      i32x4s_t r0, r1, r2, r3, r4, r5, r6, r7;
-      asm volatile(
-          "s_load_dwordx4 %0, %8, %9\n\ts_load_dwordx4 %1, %8, %10\n\t"
-          "s_load_dwordx4 %2, %8, %11\n\ts_load_dwordx4 %3, %8, %12\n\t"
-          "s_load_dwordx4 %4, %8, %13\n\ts_load_dwordx4 %5, %8, %14\n\t"
-          "s_load_dwordx4 %6, %8, %15\n\ts_load_dwordx4 %7, %8, %16\n\t"
-          "s_waitcnt lgkmcnt(0)"
-          : "=s"(r0), "=s"(r1), "=s"(r2), "=s"(r3), "=s"(r4), "=s"(r5), "=s"(r6), "=s"(r7)
-          : "s"(mrow), "i"(0), "i"(ROW * 4), "i"(2 * ROW * 4), "i"(3 * ROW * 4), "i"(4 * ROW * 4),
-            "i"(5 * ROW * 4), "i"(6 * ROW * 4), "i"(7 * ROW * 4));
-      const i32x4s_t rr[8] = {r0, r1, r2, r3, r4, r5, r6, r7};
+      const il_rows8 r8 = il_load_rows8<ROW>(mt_b + (int64_t)(e & 0xfffff) * ROW + DB);
+      const i32x4s_t rr[8] = {r8.r0, r8.r1, r8.r2, r8.r3, r8.r4, r8.r5, r8.r6, r8.r7};
       int n = 0;
 #pragma unroll
       for (int i = 0; i < CC; ++i) {
@@ -1143,9 +1156,10 @@ static const Variant kF32Variants[] = {
 // compute per staged byte the extra loaders pay off), then the float32-image
 // tilings, then the generic u16 kernel.
 static const Variant kU8Variants[] = {
-    {0, false, 8, 2, 4, 12, 8, 3, 4},   // u16 eighths, DB 48, 3 packed buffers of <= 8 channels
-                                        //   (configs[3]: 260 ms against 264 with <= 16)
-    {0, false, 8, 2, 4, 12, 8, 2, 4},   //   2 buffers (wider windows)
+    {0, false, 8, 2, 4, 12, 8, 2, 4},   // u16 eighths, DB 48, 2 packed buffers of <= 8 channels
+                                        //   (configs[3]: 236.7 ms against 239.0 with 3 buffers,
+                                        //   configs[1] u8 21.4 against 22.3, north star 119.3
+                                        //   against 121.6, once the loaders read no LDS)
     {0, false, 4, 4, 4, 8, 8, 2, 2},    // f32 image of u8 data, DB 32
     {1, true, 8, 2, 1, 8, 1, 2, 0},     // generic u16, DB 8
     {1, true, 8, 1, 1, 1, 1, 2, 0}};    // generic u16, DB 1
@@ -1173,7 +1187,6 @@ static sweep_il_fn il_kernel_for(const Variant& v) {
       v.DPW == 4)                                                                               \
     return k_sweep_il<4, 4, NCW_, NLW_, CC_, NB_>;
   if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.DPW == 4) {
-    if (v.CC == 8 && v.NBUF == 3) return k_sweep_il<2, 4, 12, 4, 8, 3, true>;
     if (v.CC == 8 && v.NBUF == 2) return k_sweep_il<2, 4, 12, 4, 8, 2, true>;
   }
   IL(14, 2, 8, 2)
@@ -1578,9 +1591,9 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
     p->dtype = dtype;
     p->n_grp = n_grp;
     if (il) {
-      // (+ CC rows of zeros: the loaders' scalar loads of a chunk's window
-      // rows read CC rows from its first channel)
-      mt_all.resize(mt_all.size() + (size_t)(v.CC * (DB + 4)), 0);
+      // (+ 8 rows of zeros: the loaders' scalar loads of a chunk's window
+      // rows read 8 rows from its first channel)
+      mt_all.resize(mt_all.size() + (size_t)(8 * (DB + 4)), 0);
       tab.swap(mt_all);
       // chunk tables [n_grp * n_dblk][1 + maxch]: count, then c0 | ncc << 20
       size_t maxch = 0;
