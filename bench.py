@@ -153,48 +153,70 @@ def _cpu_forder(x, freqs, dt, dm, orc, n=1 << 16):
                        % (dm, x.shape[0], n, el))
 
 
-_POOL_X = None
+def lease_cpus():
+    """Host CPUs this process may use: the affinity mask, capped by the
+    lease's thread budget where one is set (the GPU box exports
+    OMP_NUM_THREADS = its CPU share; nproc there shows the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
 
 
-def _pool_task(args):
-    """Reference algorithm on one channel block of one DM trial: the shifts are
-    per channel (spectra.py:54-94), so the channel sum of a trial is the sum of
-    its channel-block partial sums."""
-    from oracle import spectra_oracle as orc
-    c0, c1, bins, n_keep = args
-    sub = orc.shift_channels(_POOL_X[c0:c1].copy(), bins[c0:c1], padval=0)
-    sub[:, :n_keep].sum(axis=0)
-    return (c1 - c0) * n_keep
-
-
-def _cpu_pool(x, freqs, dt, dms, orc, workers=12, ntrials=16, cblk=64):
-    """DM-parallel multiprocessing variant: ``workers``
-    forked processes over (DM, channel block) tasks of ``ntrials`` trials.
-    12, not the box's 16-CPU share: the forked children inherit the parent's
-    GPU file descriptors and the box limits how many processes may hold the
-    card."""
-    import multiprocessing as mp
-    global _POOL_X
-    _POOL_X = x
+def _cpu_pool(x, freqs, dt, dms, orc, workers=None, ntrials=None, cblk=64):
+    """DM-parallel variant on every core of the lease: one
+    fresh interpreter per core (``python -m oracle.cpu_pool``: NumPy + the
+    oracle only, so no GPU file descriptor is inherited and the card's
+    process limit does not cap the pool), each mapping the same block from
+    a .npy in /dev/shm and running its share of (DM trial, channel block)
+    tasks of the reference algorithm; timed from one "go" to the last
+    result."""
+    import shutil
+    import tempfile
+    workers = workers or lease_cpus()
+    ntrials = ntrials or 2 * workers
     C, N = x.shape
     pick = dms[np.linspace(0, len(dms) - 1, ntrials).astype(int)]
     tasks = []
     for dm in pick:
         bins = orc.dedisperse_bins(dm, 0.0, freqs, dt)
         n_keep = N - max(0, int(bins.max()))
-        tasks += [(c, min(C, c + cblk), bins, n_keep) for c in range(0, C, cblk)]
+        tasks += [[c, min(C, c + cblk), float(dm), n_keep] for c in range(0, C, cblk)]
     workers = min(workers, len(tasks))
-    ctx = mp.get_context("fork")
-    with ctx.Pool(workers) as pool:
-        pool.map(_pool_task, tasks[:workers])  # fork + first touch, untimed
+    tmpdir = tempfile.mkdtemp(dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    procs = []
+    try:
+        path = os.path.join(tmpdir, "x.npy")
+        np.save(path, np.ascontiguousarray(x))
+        env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+        for w in range(workers):
+            p = subprocess.Popen([sys.executable, "-m", "oracle.cpu_pool"], cwd=ROOT, env=env,
+                                 stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+            p.stdin.write(json.dumps({"x": path, "freqs": list(map(float, freqs)), "dt": dt,
+                                      "tasks": tasks[w::workers]}) + "\n")
+            p.stdin.flush()
+            procs.append(p)
+        for p in procs:
+            assert p.stdout.readline().strip() == "ready", "cpu_pool worker failed"
         t0 = time.perf_counter()
-        work = sum(pool.map(_pool_task, tasks, chunksize=1))
+        for p in procs:
+            p.stdin.write("go\n")
+            p.stdin.flush()
+        res = [json.loads(p.stdout.readline()) for p in procs]
         el = time.perf_counter() - t0
-    _POOL_X = None
-    return dict(value=work / el, cores=workers,
+        for p in procs:
+            p.wait(timeout=60)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        shutil.rmtree(tmpdir, ignore_errors=True)
+    work = sum(r["work"] for r in res)
+    return dict(value=work / el, cores=workers, lease_cpus=lease_cpus(),
                 sample="%d DM trials on the same block split into %d-channel blocks over %d "
-                       "forked processes, float64 NumPy C-order, %.1f s" % (ntrials, cblk, workers,
-                                                                              el))
+                       "single-threaded worker processes (one per lease CPU), float64 NumPy "
+                       "C-order, %.1f s" % (ntrials, cblk, workers, el))
 
 
 def load_pmc(path, key):

@@ -44,9 +44,13 @@ enum { PDD_LAYOUT_TIME_MAJOR = 0, /* [nspec][nchan], filterbank file order */
 
 int pdd_version(void);
 const char* pdd_last_error(void);
-/* Free the device scratch the library keeps per stream (sweep images,
- * partial sums); synchronises the device.  Optional: the next call that
- * needs scratch allocates it again. */
+/* Free the device scratch the library keeps per (device, stream, calling host
+ * thread) -- sweep images, partial sums; synchronises the device.  Optional:
+ * the next call that needs scratch allocates it again.  Scratch is keyed by
+ * the calling thread, so several host threads may queue work on one stream
+ * (each gets its own buffers, e.g. an 8 GiB sweep image each); a thread's
+ * buffers stay allocated after it exits until this call.  Returns the first
+ * HIP error (every buffer is still freed). */
 int pdd_scratch_release(void);
 /* hipStreamSynchronize(stream) */
 int pdd_sync(void* stream);
@@ -231,9 +235,12 @@ int pdd_sweep_execute_ds(const pdd_sweep_plan* plan, const uint8_t* x8, int64_t 
  * data).  Equals pdd_sweep_execute(_grouped/_ds) of stage 1 into a
  * [n_grp2*C2][N1] subband plane followed by pdd_sweep_execute_grouped of
  * stage 2 over it (formats/spectra.py:96-138 then :229-260 per pass).
- * Returns -2, with nothing launched, for a block/grid it cannot chain (a
- * stage that needs more than one segment, or a stage-2 delay span wider than
- * an eighth of the block): run the two stages apart then. */
+ * Returns PDD_ENOCHAIN (-5), with nothing launched, for a block/grid it
+ * cannot chain (a stage that needs more than one segment, or a stage-2 delay
+ * span wider than an eighth of the block): run the two stages apart then.
+ * Any other negative status (e.g. -2: scratch allocation failed) is an
+ * error of this call. */
+#define PDD_ENOCHAIN (-5)
 int pdd_subband_chain(const pdd_sweep_plan* plan1, const void* x, int64_t n_raw, int64_t ld,
                       int64_t ds, int pad1_mode, const float* pad1vals,
                       const pdd_sweep_plan* plan2, const float* pad2vals, float* out,

@@ -23,6 +23,7 @@ F32, U8, U16 = 0, 1, 2
 PAD_VALUE, PAD_ROTATE = 0, 1
 STAT_MEAN, STAT_MEDIAN, STAT_STD, STAT_MIN, STAT_MAX = 0, 1, 2, 3, 4
 LAYOUT_TIME_MAJOR, LAYOUT_CHAN_MAJOR = 0, 1
+ENOCHAIN = -5          # pdd_subband_chain: geometry does not chain (nothing launched)
 ZDM_NONE, ZDM_INT, ZDM_WRAP = 0, 1, 2
 
 # every symbol include/pdd.h declares (checked by tests/test_abi.py)

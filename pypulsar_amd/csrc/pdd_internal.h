@@ -42,9 +42,11 @@ void set_error(const char* fmt, ...);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
-// Device scratch owned by the library, one buffer per (device, stream, slot), grown
-// with hipMalloc and kept for reuse.  Work on one stream is ordered, so
-// consecutive calls on the same stream share a slot safely; a call that
+// Device scratch owned by the library, one buffer per (device, stream, calling
+// host thread, slot), grown with hipMalloc and kept for reuse.  Work on one
+// stream is ordered and one thread queues it in program order, so
+// consecutive calls of a thread on the same stream share a slot safely (a
+// second thread on the same stream gets its own buffers); a call that
 // needs two buffers at once uses two slots.  (Replaces stream-ordered
 // hipMallocAsync/hipFreeAsync, whose pool pages, released at device
 // synchronisation, were seen to alias live hipMalloc buffers -- wrong sweep

@@ -9,6 +9,7 @@
 #include <cstdarg>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "pdd_internal.h"
@@ -28,6 +29,9 @@ namespace {
 struct ScratchBuf {
   int dev;  // the null stream is per device: key by device too
   hipStream_t st;
+  std::thread::id tid;  // per calling thread: two host threads queueing on one
+                        // stream (torch's default stream is shared) must not
+                        // interleave their launches on one buffer
   int slot;
   void* ptr;
   size_t bytes;
@@ -44,8 +48,9 @@ void* scratch(hipStream_t st, int slot, size_t bytes) {
     set_error("device scratch: hipGetDevice failed");
     return nullptr;
   }
+  const std::thread::id tid = std::this_thread::get_id();
   for (auto& b : g_scratch) {
-    if (b.dev != dev || b.st != st || b.slot != slot) continue;
+    if (b.dev != dev || b.st != st || b.tid != tid || b.slot != slot) continue;
     if (b.bytes >= bytes) return b.ptr;
     // grow: the stream's queued work may still read the old buffer
     hipError_t e = hipStreamSynchronize(st);
@@ -67,7 +72,7 @@ void* scratch(hipStream_t st, int slot, size_t bytes) {
     set_error("device scratch (%zu bytes): %s", bytes, hipGetErrorString(e));
     return nullptr;
   }
-  g_scratch.push_back({dev, st, slot, p, bytes});
+  g_scratch.push_back({dev, st, tid, slot, p, bytes});
   return p;
 }
 
@@ -1065,17 +1070,26 @@ int pdd_version(void) { return 1; }
 const char* pdd_last_error(void) { return pdd::g_err; }
 
 int pdd_scratch_release(void) {
+  // Every entry is freed and dropped even when a HIP call fails part way (a
+  // kept entry would hand out a freed pointer); the first error is returned.
   std::lock_guard<std::mutex> lock(pdd::g_scratch_mu);
+  hipError_t first = hipSuccess;
+  auto note = [&](hipError_t e) { if (first == hipSuccess && e != hipSuccess) first = e; };
   int cur = 0;
-  PDD_HIP(hipGetDevice(&cur));
+  note(hipGetDevice(&cur));
   for (auto& b : pdd::g_scratch) {
     if (!b.ptr) continue;
-    PDD_HIP(hipSetDevice(b.dev));
-    PDD_HIP(hipDeviceSynchronize());
-    (void)hipFree(b.ptr);
+    note(hipSetDevice(b.dev));
+    note(hipDeviceSynchronize());
+    note(hipFree(b.ptr));
+    b.ptr = nullptr;
   }
   pdd::g_scratch.clear();
-  PDD_HIP(hipSetDevice(cur));
+  note(hipSetDevice(cur));
+  if (first != hipSuccess) {
+    pdd::set_error("pdd_scratch_release: %s", hipGetErrorString(first));
+    return -3;
+  }
   return 0;
 }
 

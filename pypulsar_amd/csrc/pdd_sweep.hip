@@ -1761,7 +1761,7 @@ int pdd_subband_chain(const pdd_sweep_plan* p1, const void* x, int64_t n_raw, in
         il_seg_samples(p2) >= n_out)) {
     set_error("pdd_subband_chain: block of %lld samples does not chain (stage-2 span %d, "
               "one segment per stage needed)", (long long)N1, p2->max_bin);
-    return -2;  // nothing launched: run the stages apart
+    return PDD_ENOCHAIN;  // nothing launched: run the stages apart
   }
   const int64_t C2 = p2->C * p2->n_grp;
   const int64_t nR2 = 2 * Qs1 + ov;

@@ -19,6 +19,7 @@ Documented differences from the reference:
     overwriting the newer data.
 """
 import copy
+import weakref
 
 import numpy as np
 import torch
@@ -127,7 +128,11 @@ class HostView(np.ndarray):
     the device: ``__setitem__`` and in-place ufuncs on it -- or on any slice
     of it (they share its memory) -- upload the whole copy.  Reference idiom
     kept: ``chan = s.get_chan(i); chan[:] = v`` changes channel i
-    (formats/spectra.py:48-52: get_chan returns a view into self.data)."""
+    (formats/spectra.py:48-52: get_chan returns a view into self.data).
+    While the device data is unchanged, ``s.data`` / ``get_chan`` /
+    ``get_spectrum`` hand out views of ONE host copy (as the reference's
+    views share ``self.data``), so writes through two open views both land;
+    a view taken before a device-side change raises on write."""
 
     def __array_finalize__(self, obj):
         self._root = getattr(obj, "_root", None)
@@ -205,10 +210,17 @@ class Spectra(object):
     @property
     def data(self):
         """float64 host copy of the data that writes through to the device
-        (HostView)."""
+        (HostView).  One copy per device version, shared by every view taken
+        while the device data is unchanged (weakly cached)."""
+        ref = getattr(self, "_host", None)
+        if ref is not None and ref[0] == self._version:
+            v = ref[1]()
+            if v is not None:
+                return v
         v = self._x.to(torch.float64).cpu().numpy().view(HostView)
         v._root = v
         v._owner = (self, self._version)
+        self._host = (self._version, weakref.ref(v))
         return v
 
     @data.setter
@@ -218,7 +230,9 @@ class Spectra(object):
         self._version = getattr(self, "_version", 0) + 1
 
     def _upload_host(self, arr):
-        """Write a full [numchans, numspectra] host array back (HostView)."""
+        """Write a full [numchans, numspectra] host array back (HostView).
+        The device now equals the shared host copy, so the version (and the
+        copy's validity) is unchanged."""
         assert arr.shape == tuple(self._x.shape)
         self._x.copy_(torch.from_numpy(np.ascontiguousarray(arr, dtype=np.float32)))
         self._raw8 = None
@@ -250,6 +264,7 @@ class Spectra(object):
     def __deepcopy__(self, memo):
         other = copy.copy(self)
         other._version = 0
+        other._host = None  # never share the original's host copy
         other._x = self._x.clone()
         other._raw8 = None if self._raw8 is None else self._raw8.clone()
         other.freqs = copy.deepcopy(self.freqs, memo)

@@ -470,11 +470,11 @@ class DDplanExecutor(object):
                         g1._plan, ptr(raw8), self.N, raw8.stride(0), s.ds, _lib.PAD_VALUE,
                         ptr(pv1), s.g2._plan, ptr(pv2), ptr(s.plane), s.plane.stride(0),
                         s.n_out, s.per, 1, stream_ptr())
-                    if rc != -2:
-                        _lib.check(rc, "pdd_subband_chain")
+                    if rc != _lib.ENOCHAIN:
+                        _lib.check(rc, "pdd_subband_chain")   # errors (e.g. -2 OOM) raise
                         results.append((s.step, s.step.DMs, s.plane[:, :s.n_out]))
                         continue
-                    # -2: a geometry the chain does not take (nothing was
+                    # a geometry the chain does not take (nothing was
                     # launched): run the stages apart from now on
                     s.chain = False
             if s.sub is None:

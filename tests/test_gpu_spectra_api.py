@@ -56,3 +56,34 @@ def test_stale_view_raises_and_ops_see_writes(gpu):
     np.testing.assert_array_equal(s.data, want)
     # reading does not disturb anything
     assert float(np.asarray(s.data).sum()) == float(want.sum())
+
+
+@pytest.mark.gpu
+def test_two_open_views_both_write_through(gpu):
+    """two views taken while the device data is unchanged share one
+    host copy (the reference's get_chan views share self.data), so writing
+    through the first and then the second keeps BOTH writes; a deep copy never
+    shares the original's host copy."""
+    import copy
+    from pypulsar_amd.formats.spectra import Spectra
+    C, N = 8, 512
+    x = u8_data(C, N, 9)
+    s = Spectra(band(C), DT, x)
+    a = s.get_chan(0)
+    b = s.get_chan(1)
+    a[:] = 0.0
+    b[:] = 0.0
+    want = x.astype(np.float64)
+    want[:2] = 0.0
+    np.testing.assert_array_equal(s.data, want)
+    d = copy.deepcopy(s)
+    d.get_chan(2)[:] = 3.0
+    np.testing.assert_array_equal(s.data, want)          # the original is untouched
+    want_d = want.copy()
+    want_d[2] = 3.0
+    np.testing.assert_array_equal(d.data, want_d)
+    sp = s.get_spectrum(5)
+    sp[:] = 1.0
+    want[:, 5] = 1.0
+    np.testing.assert_array_equal(s.get_chan(3), want[3])
+    np.testing.assert_array_equal(s.data, want)
