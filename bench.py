@@ -44,11 +44,16 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# MI355X peaks (MI355X_MICROARCH.md §Chip-level parameters)
+# MI355X peaks (MI355X_MICROARCH.md §Chip-level parameters, §LDS)
 PEAK_HBM_GBS = 8000.0
-PEAK_ADD_T = 78.6   # VALU adds: 256 CU x 2.4 GHz x 128 (v_pk_add_f32 / two u16 lanes per v_add_u32)
 CLK_GHZ = 2.4
 N_CU = 256
+# LDS ds_read_b128: 256 B/clk/CU (MI355X_MICROARCH.md §LDS table)
+LDS_B_PER_CLK = 256
+# VALU: 4 SIMD-32 per CU, a wave64 instruction over 2 cycles (MI355X_MICROARCH.md
+# :53-54) = 128 lane-ops/clk/CU = 78.6 T lane-ops/s chip-wide
+VALU_LANE_OPS_T = N_CU * 4 * 32 * CLK_GHZ / 1e3
+PEAK_ADD_T = VALU_LANE_OPS_T * 2   # v_pk_add_f32 / v_add_u32 on packed u16: 2 adds per lane-op
 
 CONFIGS = {
     # BASELINE.json configs[3] (the metric's configuration): DM-sharded node sweep
@@ -261,14 +266,21 @@ def main():
     ap.add_argument("--gather", action="store_true",
                     help="dmshard: also gather every batch's plane rows to rank 0 (p2p)")
     ap.add_argument("--zdm", default="auto", choices=["auto", "int", "wrap", "float", "none"],
-                    help="stream: zero-DM mode (auto = exact integer 16-bit path for 8-bit data)")
+                    help="stream: zero-DM mode (auto = 'wrap', the reference's uint8 result of "
+                         "zero_dm_filter.py:30-39, on the exact 16-bit path)")
     ap.add_argument("--cpu-trials", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="dmshard: skip the PCIe-inclusive (pinned host -> H2D -> step) leg")
     ap.add_argument("--e2e", action="store_true",
                     help="also time one PCIe-inclusive step: pinned host block -> H2D -> "
                          "sweep -> D2H of the plane into pinned host memory")
     ap.add_argument("--search", action="store_true",
                     help="stream: also boxcar-search every block (StreamingSearch)")
+    ap.add_argument("--rehearse", type=int, default=0, metavar="W",
+                    help="dmshard: run every rank of a W-GPU step on this one GPU (its own "
+                         "slice's corner turn + its DM slice) and report per-rank times and the "
+                         "predicted compute efficiency")
     args = ap.parse_args()
     _maybe_spawn(args)
 
@@ -299,6 +311,8 @@ def main():
         return search_bench(args, cfg, rank, world, dev)
     if args.config == "ops":
         return ops_bench(args, cfg, rank, world, dev)
+    if args.rehearse:
+        return rehearse_bench(args, cfg, dev)
     return sweep_bench(args, cfg, rank, world, dev)
 
 
@@ -360,6 +374,40 @@ def sweep_bench(args, cfg, rank, world, dev):
     if sw is not None:
         sw.set_timing(False)
     e2e = None
+    if mode == "dmshard" and not args.no_e2e:
+        # PCIe-inclusive: this rank's slices of the block in
+        # pinned host memory -> H2D -> the step; planes stay resident (the
+        # consumer is the on-device search), so no plane D2H
+        hpart = torch.empty(part.shape, dtype=part.dtype, pin_memory=True)
+        hpart.copy_(part)
+        ms, h2d = [], []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t1 = time.perf_counter()
+            part.copy_(hpart, non_blocking=True)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            step()
+            torch.cuda.synchronize()
+            t3 = time.perf_counter()
+            ms.append((t3 - t1) * 1e3)
+            h2d.append((t2 - t1) * 1e3)
+        del hpart
+        best = min(ms)
+        if world > 1:
+            t = torch.tensor([best], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            best = float(t.item())
+        nbytes = part.numel() * part.element_size()
+        e2e = {"ms_per_step": best, "value": D * n_out * C / (best * 1e-3),
+               "h2d_ms": min(h2d), "h2d_GBs": nbytes / (min(h2d) * 1e-3) / 1e9,
+               "bytes_h2d_per_rank": nbytes, "bytes_d2h": 0,
+               "note": "best of 3 (max over ranks): pinned host slices -> H2D (this rank's 1/N "
+                       "of every time batch) -> the step; planes stay resident per rank (the "
+                       "consumer is the on-device search), so nothing returns over PCIe; the "
+                       "H2D is not overlapped with the sweep here"}
     if args.e2e and mode == "timeblock":
         # PCIe-inclusive: the boundary handed host buffers
         hx = torch.empty(x.shape, dtype=x.dtype, pin_memory=True)
@@ -389,9 +437,13 @@ def sweep_bench(args, cfg, rank, world, dev):
     value = units_all * steps / el
     s_in = 1 if dtype == "u8" else 4
     achieved = adds_rank_step * steps / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else None
-    # LDS roof: ds_read_b128 at 256 B/clk/CU feeds 4 f32 samples (f32 path)
-    # or 8 u16 samples (8-bit path) per 16 B
-    lds_roof = N_CU * CLK_GHZ * 1e9 * 256 / 16 * (8 if dtype == "u8" else 4) / 1e12
+    # LDS roof (the binding one): ds_read_b128 at 256 B/clk/CU
+    # feeds 4 f32 samples (f32 quarters) or 8 u16 samples (u16 eighths) per 16 B
+    lds_roof = N_CU * CLK_GHZ * 1e9 * LDS_B_PER_CLK / 16 * (8 if dtype == "u8" else 4) / 1e12
+    # VALU roof: u16 eighths add two channels of two packed samples per
+    # v_add3_u32 lane-op (4 adds); f32 quarters two samples per v_pk_add_f32
+    valu_adds = 4 if dtype == "u8" else 2
+    valu_roof = VALU_LANE_OPS_T * valu_adds
     uniq_bytes = C * N * s_in + rows * n_out * 4
     k_s = kern_ms * 1e-3 / steps if kern_ms > 0 else None
     pmc_key = "%s_%s" % (args.config, dtype)
@@ -428,8 +480,8 @@ def sweep_bench(args, cfg, rank, world, dev):
                        "n_out": n_out, "parallelism": "%s%d" % ("tb" if mode == "timeblock"
                                                                 else "dm", world),
                        "rccl_world_size": rccl_world, "plan": plan},
-            "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_ADD_T,
-                         "unit": "T adds/s", "frac": achieved / PEAK_ADD_T if achieved else None,
+            "roofline": {"bound": "lds", "achieved": achieved, "peak": lds_roof,
+                         "unit": "T adds/s", "frac": achieved / lds_roof if achieved else None,
                          "traffic": traffic,
                          "traffic_source": ("profiles/pmc_sweep.json[%s] (separate rocprofv3 "
                                             "--pmc FETCH_SIZE / WRITE_SIZE passes of this "
@@ -439,12 +491,18 @@ def sweep_bench(args, cfg, rank, world, dev):
                          "launches_per_step": launches / steps if launches else None,
                          "kernel_s_per_step": k_s,
                          "adds_per_step_rank0": adds_rank_step,
-                         "note": "the sweep does one FP32/integer add per samp*ch*DM and no "
-                                 "MFMA-shaped work; its binding roof is the VALU add rate "
-                                 "(v_pk_add_f32 / two u16 lanes per v_add_u32), with the LDS "
-                                 "read roof beside it (DESIGN.md §3-4)",
-                         "lds_roof": lds_roof,
-                         "frac_lds_roof": achieved / lds_roof if achieved else None},
+                         "note": "one add per samp*ch*DM, no MFMA-shaped work; every add reads "
+                                 "its sample from the LDS image (ds_read_b128: %d samples per 16 B "
+                                 "at 256 B/clk/CU = the peak, in adds/s), which binds; the VALU "
+                                 "issue rate (SIMD-32, MI355X_MICROARCH.md:53-54) is beside it "
+                                 "(DESIGN.md §3-4)" % (8 if dtype == "u8" else 4),
+                         "lds_bytes_per_add": 2 if dtype == "u8" else 4,
+                         "valu": {"peak": valu_roof, "unit": "T adds/s",
+                                  "instr": ("v_add3_u32 over a channel pair of packed u16 samples "
+                                            "(4 adds per lane-op)" if dtype == "u8" else
+                                            "v_pk_add_f32 (2 adds per lane-op)"),
+                                  "lane_ops_T": VALU_LANE_OPS_T,
+                                  "frac": achieved / valu_roof if achieved else None}},
             "roofline_hbm": {"bound": "hbm", "achieved": uniq_bytes / k_s / 1e9 if k_s else None,
                              "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": uniq_bytes / k_s / 1e9 / PEAK_HBM_GBS if k_s else None,
@@ -470,6 +528,98 @@ def sweep_bench(args, cfg, rank, world, dev):
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def rehearse_bench(args, cfg, dev):
+    """The W-rank DM-sharded step (BASELINE configs[3] by default) rehearsed on
+    ONE GPU: first the whole grid as one rank (the N=1 step), then rank r =
+    0..W-1 exactly as it runs in a W-GPU job (DMShardedSweep(world=W,
+    rank=r): its own slice of each of the 4 time batches corner-turned into
+    the pieces block, its DDplan-work-balanced DM slice -- DDplan2b.py:272-273
+    -- swept at the global width), the all-gathers replaced by a block that
+    already holds every rank's slices.  Reports per-rank step and sweep-kernel
+    times, trial-block rounding and the predicted compute-side efficiency
+    t(1 GPU) / (W * max_r t_r); the exchange (all-gathers over xGMI) is not
+    part of it and is modelled in DESIGN.md §5."""
+    from pypulsar_amd.sharding import DMShardedSweep, split_block, trial_work
+    W = args.rehearse
+    C, N, D = cfg["C"], cfg["N"], cfg["D"]
+    dtype = args.dtype or cfg["dtype"]
+    tdt = torch.uint8 if dtype == "u8" else torch.float32
+    dt = 64e-6
+    freqs = band(C)
+    dms = np.linspace(cfg["dm_lo"], cfg["dm_hi"], D)
+    nb = args.batches or 4
+    steps = args.steps if args.steps is not None else 3
+    warmup = args.warmup if args.warmup is not None else 1
+    block = synth_block(N, C, 1000, dtype, dev)            # time-major [N, C], file order
+
+    def timed(ds, part):
+        for _ in range(warmup):
+            ds(part)
+        torch.cuda.synchronize()
+        ds.sw.set_timing(True)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            ds(part)
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) / steps * 1e3
+        kms, launches = ds.sw.timing_read()
+        ds.sw.set_timing(False)
+        return el, kms / steps, launches // steps
+
+    # the N = 1 step (whole grid, one rank, nb = 1 as in the default bench line)
+    ds1 = DMShardedSweep(dms, freqs, dt, N, dtype=tdt, n_batches=1, work=trial_work(dms, 1),
+                         device=dev)
+    t1, k1, l1 = timed(ds1, block.view(1, N, C))
+    db = ds1.sw.info(1 if dtype == "u8" else 0)["dms_per_block"]
+    ds1.close()
+    del ds1
+    torch.cuda.empty_cache()
+    log("rehearse: 1 GPU step %.1f ms (sweep %.1f ms, %d launches)" % (t1, k1, l1))
+    ranks, shared = [], None
+    for r in range(W):
+        ds = DMShardedSweep(dms, freqs, dt, N, dtype=tdt, n_batches=nb, work=trial_work(dms, 1),
+                            device=dev, world=W, rank=r, x_buf=shared)
+        if shared is None:
+            ds.prefill(block)
+            shared = ds.x
+        part = split_block(block, nb, W, r)
+        t, k, l = timed(ds, part)
+        blocks = -(-ds.rows // db)
+        ranks.append({"rank": r, "dms": [ds.lo, ds.hi], "rows": ds.rows, "step_ms": t,
+                      "sweep_kernel_ms": k, "launches": l, "trial_blocks": blocks,
+                      "trial_block_fill": ds.rows / (blocks * db)})
+        log("rehearse: rank %d/%d DMs [%d, %d) step %.1f ms (sweep %.1f ms)"
+            % (r, W, ds.lo, ds.hi, t, k))
+        ds.close()
+        del ds, part
+        torch.cuda.empty_cache()
+    tmax = max(x["step_ms"] for x in ranks)
+    line = {
+        "metric": "rehearsal of the %d-GPU DM-sharded step on one GPU (compute side)" % W,
+        "value": t1 / (W * tmax), "unit": "predicted compute efficiency t1 / (W * max_r t_r)",
+        "n_gpus": 1, "rehearsed_world": W, "steps": steps, "warmup": warmup,
+        "higher_is_better": True, "dtype": dtype,
+        "config": {"workload": "%d ch x 2^%d x %d DM (%g-%g pc/cc), %d time batches, pieces "
+                               "layout (P = N / (batches * W) = %d)"
+                               % (C, int(np.log2(N)), D, cfg["dm_lo"], cfg["dm_hi"], nb,
+                                  N // (nb * W)),
+                   "config_name": args.config, "dms_per_trial_block": db},
+        "one_gpu": {"step_ms": t1, "sweep_kernel_ms": k1, "launches": l1},
+        "ranks": ranks,
+        "max_rank_step_ms": tmax,
+        "mean_rank_step_ms": float(np.mean([x["step_ms"] for x in ranks])),
+        "max_over_mean": tmax / float(np.mean([x["step_ms"] for x in ranks])),
+        "predicted_step_ms_at_W": tmax,
+        "note": "all-gathers replaced by a pre-filled block: exchange time excluded "
+                "(DESIGN.md §5 models it: batch k+1's all-gather overlaps batch k's sweep, "
+                "only the first batch's is exposed)",
+    }
+    from pypulsar_amd.delays import sweep_table
+    n_out = N - int(sweep_table(dms[-1:], freqs, dt).max())
+    line["predicted_value_at_W"] = D * n_out * C / (tmax * 1e-3)
+    print(json.dumps(line), flush=True)
 
 
 def _finish(args, world, line):
@@ -722,6 +872,7 @@ def stream_bench(args, cfg, rank, world, dev):
         el = float(t.item())
     units = D * nb * C * args.steps * world
     value = units / el
+    lds_roof = N_CU * CLK_GHZ * 1e9 * LDS_B_PER_CLK / 16 * (8 if st.exact else 4) / 1e12
     ms = el / args.steps * 1e3
     in_rate = block * args.steps * world / el  # input spectra per second
     line = {
@@ -736,15 +887,23 @@ def stream_bench(args, cfg, rank, world, dev):
                                   "exact u16" if st.exact else "float32",
                                   " + boxcar search (13 widths, S/N 8)" if args.search else ""),
                    "candidates": ncand if args.search else None,
+                   "zero_dm_semantics": {"wrap": "the reference's own: uint8 (x - round(mean)) "
+                                                 "mod 256, zero_dm_filter.py:30-39",
+                                         "int": "the reference's rounding without the uint8 wrap",
+                                         "float": "x - mean in float32 (the reference's float "
+                                                  "data semantics)",
+                                         "none": "no filter"}[st.mode],
+                   "u16_flush_channels": (min(256, 65535 // st.input_max) if st.exact else None),
                    "config_name": "stream", "channels": C, "block": block, "overlap": st.ov,
                    "downsamp": ds, "dm_trials": D, "parallelism": "tb%d" % world},
         "realtime_factor": (block * dt) / (ms * 1e-3),
         "input_spectra_per_s": in_rate,
-        "roofline": {"bound": "valu", "achieved": D * nb * C / (ms * 1e-3) / 1e12,
-                     "peak": PEAK_ADD_T, "unit": "T adds/s",
-                     "frac": D * nb * C / (ms * 1e-3) / 1e12 / PEAK_ADD_T, "traffic": None,
+        "roofline": {"bound": "lds", "achieved": D * nb * C / (ms * 1e-3) / 1e12,
+                     "peak": lds_roof, "unit": "T adds/s",
+                     "frac": D * nb * C / (ms * 1e-3) / 1e12 / lds_roof, "traffic": None,
                      "note": "whole-step time (H2D, prologue, sweep) per block; one add per "
-                             "unit against the VALU add roof"},
+                             "unit against the sweep's LDS read roof (%s image)"
+                             % ("u16 eighths" if st.exact else "float32 quarters")},
         "cpu_baseline": None,
     }
     st.close()

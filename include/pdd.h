@@ -248,6 +248,13 @@ int pdd_subband_chain(const pdd_sweep_plan* plan1, const void* x, int64_t n_raw,
 /* Extents used by the plan (for DESIGN/bench reporting): DM trials, channels,
  * DMs per block, time samples per block, LDS bytes per workgroup. */
 int pdd_sweep_plan_info(const pdd_sweep_plan* plan, int64_t* info /*[8]*/);
+/* Integer-input plans (PDD_U8, PDD_U16): the largest sample value the
+ * caller's input (and integer pads) can hold, default 255 / 1023.  The
+ * sweep adds two samples per 32-bit lane pair and converts every
+ * floor(65535 / max_value) channels (at most 256), so a tighter bound means
+ * fewer conversions; a sample above it gives wrong sums.  E.g. the
+ * zero_dm_filter.py:30-39 uint8-wrap image co-added by 2 is <= 510. */
+int pdd_sweep_plan_set_input_max(pdd_sweep_plan* plan, int max_value);
 int pdd_sweep_plan_destroy(pdd_sweep_plan* plan);
 /* Measurement hooks (bench.py): with timing on, every sweep-kernel launch
  * of pdd_sweep_execute(_grouped) -- not the interleave pre-pass -- is

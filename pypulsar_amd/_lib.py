@@ -31,6 +31,7 @@ EXPORTS = (
     "pdd_version", "pdd_last_error", "pdd_sync", "pdd_corner_turn", "pdd_convert_f32",
     "pdd_channel_stats", "pdd_shift_pad", "pdd_shift_group_sum", "pdd_downsample",
     "pdd_zero_dm", "pdd_sweep_plan_create", "pdd_sweep_execute", "pdd_sweep_plan_info",
+    "pdd_sweep_plan_set_input_max",
     "pdd_sweep_plan_destroy", "pdd_global_stats", "pdd_scale_rows", "pdd_masked_fill",
     "pdd_smooth", "pdd_zdm_downsample", "pdd_sweep_set_timing", "pdd_sweep_kernel_ms",
     "pdd_sweep_plan_create_grouped", "pdd_sweep_execute_grouped", "pdd_sp_chunk_stats",
@@ -71,6 +72,7 @@ _SIGS = {
     "pdd_sweep_execute_ex": ([_vp, _vp, _i64, _i64, _i64, _i64, _int, _vp, _vp, _i64, _i64,
                               ctypes.c_float, _vp], _int),
     "pdd_sweep_plan_info": ([_vp, _vp], _int),
+    "pdd_sweep_plan_set_input_max": ([_vp, _int], _int),
     "pdd_sweep_plan_destroy": ([_vp], _int),
     "pdd_global_stats": ([_vp, _i64, _i64, _i64, _vp, _vp], _int),
     "pdd_scale_rows": ([_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp], _int),

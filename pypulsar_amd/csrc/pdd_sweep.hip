@@ -906,7 +906,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   // u16 elements (8-bit data): 8 eighth samples per read as packed u16 pairs,
   // accumulated with plain 32-bit adds (two u16 lanes per add, no carry while
   // <= 257 channels of values <= 255 are summed) and flushed to float every
-  // flush_n channels (256 for 8-bit data, 64 for 16-bit data <= 1023) --
+  // flush_n channels (floor(65535 / the plan's input bound), at most 256) --
   // exact.
   // accumulators as float pairs: the adds issue as v_pk_add_f32 (two samples
   // per VALU instruction: half the issue slots of scalar v_add_f32)
@@ -1268,6 +1268,7 @@ struct pdd_sweep_plan {
   uint8_t* d_rows = nullptr;
   int rows_max = 0, nchunk = 0;
   int dtype = PDD_F32;     // input element type
+  int input_max = 0;       // largest input value (integer input; 0 = the dtype's bound)
   int64_t n_grp = 1;       // independent channel groups (grouped sweep)
   // timing of the sweep kernel (pdd_sweep_set_timing): one event pair per
   // bracketed launch, recorded on the execute stream without host syncs
@@ -1321,8 +1322,11 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
   const int SP = p->v.S;  // samples per element: 4 (float32 quarters) or 8 (u16 eighths)
   const bool u16 = (SP == 8);
   PDD_REQUIRE(!u16 || p->dtype != PDD_F32, "pdd_sweep_execute: u16 path needs integer input");
-  // packed u16 lanes: 257 channels of 8-bit values, 64 of 16-bit values <= 1023
-  const int flush_n = p->dtype == PDD_U8 ? 256 : 64;
+  // packed u16 lanes hold floor(65535 / max value) channel sums: 257 channels
+  // of 8-bit values, 64 of 16-bit values <= 1023, 128 of the wrap-mode
+  // zero-DM image downsampled by 2 (<= 510; pdd_sweep_plan_set_input_max)
+  const int vmax = p->input_max > 0 ? p->input_max : (p->dtype == PDD_U8 ? 255 : 1023);
+  const int flush_n = std::min(256, 65535 / vmax);
   const int64_t C = p->C * p->n_grp;  // all channels (groups are contiguous channel ranges)
   const int64_t lo = std::min(0, p->min_bin), hi = std::max(0, p->max_bin);
   int64_t seg = il_seg_samples(p);  // output samples per segment
@@ -1786,6 +1790,16 @@ int pdd_subband_chain(const pdd_sweep_plan* p1, const void* x, int64_t n_raw, in
                     n_out, row_g, row_d, 0.f, stream, e2);
   }
   return rc;
+}
+
+int pdd_sweep_plan_set_input_max(pdd_sweep_plan* p, int max_value) {
+  PDD_REQUIRE(p, "pdd_sweep_plan_set_input_max: null pointer");
+  PDD_REQUIRE(p->dtype != PDD_F32, "pdd_sweep_plan_set_input_max: integer-input plans only");
+  const int bound = p->dtype == PDD_U8 ? 255 : 1023;
+  PDD_REQUIRE(max_value >= 1 && max_value <= bound,
+              "pdd_sweep_plan_set_input_max: %d outside [1, %d]", max_value, bound);
+  p->input_max = max_value;
+  return 0;
 }
 
 int pdd_sweep_set_timing(pdd_sweep_plan* p, int on) {

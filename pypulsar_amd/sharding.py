@@ -152,15 +152,29 @@ class DMShardedSweep(object):
     dms_slice, out, n_cols)`` (piece 0: x channel-major [C, N]) are injected
     by the CPU tests; the defaults are pdd_corner_turn and the HIP DMSweep of
     this rank's slice (built once).
+
+    Rehearsal (``world=W, rank=r`` given; no process group needed): the
+    exact compute of rank r of a W-rank run -- its own slice's corner turn
+    into the block, its DM slice swept at the global width, batch by batch
+    -- on one device, with the exchange replaced by a block that already
+    holds every rank's slices (``prefill`` once, or a shared ``x_buf``).
+    Stacking the W ranks' planes gives the one-shot plane; timing each rank
+    gives the compute side of the W-GPU step (``bench.py --rehearse W``).
     """
 
     def __init__(self, dms, freqs, dt, N, dtype=torch.uint8, n_batches=1, work=None,
                  gather=False, dst=0, group=None, device=None, to_cm=None, sweep_fn=None,
-                 pieces=None):
+                 pieces=None, world=None, rank=None, x_buf=None):
         from . import delays as _delays
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.rehearse = world is not None
+        if self.rehearse:
+            self.world, self.rank = int(world), int(rank)
+            assert 0 <= self.rank < self.world, "rank outside the rehearsed world"
+            assert not gather, "a rehearsal has no plane gather (one device)"
+        else:
+            self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+            self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.dms = np.asarray(dms, dtype=np.float64)
         self.freqs = np.asarray(freqs, dtype=np.float64)
         self.C = len(self.freqs)
@@ -194,18 +208,22 @@ class DMShardedSweep(object):
         self.gather = bool(gather)
         self.dst = dst
         # buffers (reused every call)
+        xshape = (self.N // self.P, self.C, self.P) if self.pieces else (self.C, self.N)
+        if x_buf is not None:
+            assert tuple(x_buf.shape) == xshape and x_buf.dtype == dtype and x_buf.is_contiguous()
+            self.x = x_buf
+        else:
+            self.x = torch.empty(xshape, dtype=dtype, device=self.device)
         if self.pieces:
             # two corner-turn buffers: batch k+1's turn must not overwrite the
             # one batch k's all-gather may still be reading
-            self.cm = [torch.empty((self.C, self.P), dtype=dtype, device=self.device)
-                       for _ in range(2)]
-            self.x = torch.empty((self.N // self.P, self.C, self.P), dtype=dtype,
-                                 device=self.device)
+            self.cm = ([] if self.rehearse else
+                       [torch.empty((self.C, self.P), dtype=dtype, device=self.device)
+                        for _ in range(2)])
             self.xt = None
         else:
             self.xt = (torch.empty((self.N, self.C), dtype=dtype, device=self.device)
-                       if self.world > 1 else None)
-            self.x = torch.empty((self.C, self.N), dtype=dtype, device=self.device)
+                       if self.world > 1 and not self.rehearse else None)
         cols = [edges[k + 1] - edges[k] for k in range(self.nb)]
         if self.gather and self.rank == self.dst:
             # dst's full batch planes; its own rows are views of them
@@ -235,51 +253,71 @@ class DMShardedSweep(object):
         """Run one pipelined sweep of the block whose per-rank slices are
         ``part`` ([n_batches, P, C]).  Returns this rank's batch planes
         (with ``gather``: the full [D, cols_k] batch planes on ``dst``)."""
-        nb, W, T, P = self.nb, self.world, self.T, self.P
-        assert tuple(part.shape) == (nb, P, self.C) and part.dtype == self.dtype
+        nb = self.nb
+        assert tuple(part.shape) == (nb, self.P, self.C) and part.dtype == self.dtype
         sends = []
-
-        def exchange(k):
-            """Batch k into x: (corner turn +) all-gather; returns the pending
-            collective (None when done)."""
-            if self.pieces:
-                dst = self.x[k * W:(k + 1) * W]  # [W, C, P]
-                if W == 1:
-                    self.to_cm(part[k], dst[0])
-                    return None
-                cm = self.cm[k % 2]
-                self.to_cm(part[k], cm)
-                return _all_gather_into(dst.view(W * self.C, P), cm, group=self.group,
-                                        async_op=True)
-            if W == 1:
-                self.to_cm(part[k], self.x[:, k * T:(k + 1) * T])
-                return None
-            return _all_gather_into(self.xt[k * T:(k + 1) * T], part[k], group=self.group,
-                                    async_op=True)
-
-        def sweep(k):
-            if not self.pieces and W > 1:
-                self.to_cm(self.xt[k * T:(k + 1) * T], self.x[:, k * T:(k + 1) * T])
-            a, b = self.col_edges[k], self.col_edges[k + 1]
-            if self.rows and b > a:
-                self.sweep_fn(self.x, self.N, P if self.pieces else 0, a,
-                              self.dms[self.lo:self.hi], self.planes[k], b - a)
-            if self.gather:
-                sends.extend(self._gather_batch(k))
-
         pending = [None] * nb
         for k in range(nb):
-            pending[k] = exchange(k)      # batch k's exchange overlaps batch k-1's sweep
+            pending[k] = self.exchange_batch(part, k)  # overlaps batch k-1's sweep
             if k > 0:
                 if pending[k - 1] is not None:
                     pending[k - 1].wait()
-                sweep(k - 1)
+                sends.extend(self.sweep_batch(k - 1))
         if pending[nb - 1] is not None:
             pending[nb - 1].wait()
-        sweep(nb - 1)
+        sends.extend(self.sweep_batch(nb - 1))
         for w in sends:
             w.wait()
         return self.full if (self.gather and self.rank == self.dst) else self.planes
+
+    def exchange_batch(self, part, k):
+        """Batch k into x: this rank's corner turn (+ the async all-gather of
+        every rank's slice); returns the pending collective or None."""
+        W, T, P = self.world, self.T, self.P
+        if self.rehearse:
+            # this rank's own slice only; the others' are already in x
+            r = self.rank
+            if self.pieces:
+                self.to_cm(part[k], self.x[k * W + r])
+            else:
+                self.to_cm(part[k], self.x[:, k * T + r * P:k * T + (r + 1) * P])
+            return None
+        if self.pieces:
+            dst = self.x[k * W:(k + 1) * W]  # [W, C, P]
+            if W == 1:
+                self.to_cm(part[k], dst[0])
+                return None
+            cm = self.cm[k % 2]
+            self.to_cm(part[k], cm)
+            return _all_gather_into(dst.view(W * self.C, P), cm, group=self.group,
+                                    async_op=True)
+        if W == 1:
+            self.to_cm(part[k], self.x[:, k * T:(k + 1) * T])
+            return None
+        return _all_gather_into(self.xt[k * T:(k + 1) * T], part[k], group=self.group,
+                                async_op=True)
+
+    def sweep_batch(self, k):
+        """Sweep plane columns of batch k (its exchange complete); returns the
+        pending plane sends (``gather``)."""
+        W, T = self.world, self.T
+        if not self.pieces and W > 1 and not self.rehearse:
+            self.to_cm(self.xt[k * T:(k + 1) * T], self.x[:, k * T:(k + 1) * T])
+        a, b = self.col_edges[k], self.col_edges[k + 1]
+        if self.rows and b > a:
+            self.sweep_fn(self.x, self.N, self.P if self.pieces else 0, a,
+                          self.dms[self.lo:self.hi], self.planes[k], b - a)
+        return self._gather_batch(k) if self.gather else []
+
+    def prefill(self, block_tc):
+        """Rehearsal: write the WHOLE time-major [N, C] block into x, as the
+        all-gathers of every rank would (once, outside any timing)."""
+        assert tuple(block_tc.shape) == (self.N, self.C) and block_tc.dtype == self.dtype
+        if self.pieces:
+            for b in range(self.N // self.P):
+                self.to_cm(block_tc[b * self.P:(b + 1) * self.P], self.x[b])
+        else:
+            self.to_cm(block_tc, self.x)
 
     def _gather_batch(self, k):
         """Rows of batch k to ``dst`` (point-to-point, async): dst receives each

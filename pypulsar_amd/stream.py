@@ -5,8 +5,8 @@ sweep, with pinned-host H2D copies overlapped with compute.
 Zero-DM modes (bin/zero_dm_filter.py:30-39 subtracts each spectrum's channel
 mean; for integer data the mean is rounded half-to-even and the difference is
 taken in the data dtype):
-  * ``"auto"`` (default): ``"int"`` where the exact path applies, else
-    ``"float"``.
+  * ``"auto"`` (default): ``"wrap"`` -- the reference's uint8 result --
+    where the exact path applies (8-bit input), else ``"float"``.
   * ``"int"`` (8-bit input, downsamp <= 2): x - round(mean) as an
     exact signed integer (the reference's rounding without the uint8 wrap),
     co-added and offset into 16-bit samples <= 1023 (pdd_zdm_int_downsample)
@@ -81,7 +81,9 @@ class StreamingSweep(object):
         self.dt = dt
         mode = {True: "float", False: "none"}.get(zero_dm, zero_dm)
         if mode == "auto":
-            mode = "int" if (dtype == torch.uint8 and self.C % 16 == 0 and self.ds <= 2) else "float"
+            # the reference's own result for 8-bit data: uint8 wrap
+            # (zero_dm_filter.py:30-39), exact on the 16-bit path
+            mode = "wrap" if (dtype == torch.uint8 and self.C % 16 == 0 and self.ds <= 4) else "float"
         if mode not in ("int", "wrap", "float", "none"):
             raise ValueError("zero_dm must be 'auto', 'int', 'wrap', 'float', True or False")
         self.dtype = dtype
@@ -95,7 +97,11 @@ class StreamingSweep(object):
         self.mode = mode
         self.zero_dm = mode != "none"
         self.offset = 255 * self.ds if mode == "int" else 0
-        self.sweep = DMSweep(dms, self.freqs, dt * self.ds, dtype="u16" if self.exact else "f32")
+        # bound of the 16-bit image: offset + co-added (x - round(mean)) for
+        # "int" (<= 510 ds), co-added bytes for "wrap" / "none" (<= 255 ds)
+        self.input_max = (510 if mode == "int" else 255) * self.ds if self.exact else None
+        self.sweep = DMSweep(dms, self.freqs, dt * self.ds, dtype="u16" if self.exact else "f32",
+                             input_max=self.input_max)
         self.D = self.sweep.D
         self.max_bin = max(0, self.sweep.max_bin)
         self.block = int(block)

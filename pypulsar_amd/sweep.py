@@ -58,7 +58,11 @@ class DMSweep(object):
     [C, N] device tensor of that dtype (int16 / uint16 storage for 'u16') or
     a ``Spectra``."""
 
-    def __init__(self, dms, freqs, dt, cur_dm=0.0, dtype="f32"):
+    def __init__(self, dms, freqs, dt, cur_dm=0.0, dtype="f32", input_max=None):
+        """``input_max`` (integer dtypes): the largest sample value the input
+        and its integer pads hold (default 255 for 'u8', 1023 for 'u16'); a
+        tighter bound lets the exact packed-u16 accumulation convert less
+        often (pdd_sweep_plan_set_input_max)."""
         _lib.require_gpu()
         self.dms = np.atleast_1d(np.asarray(dms, dtype=np.float64))
         self.freqs = np.asarray(freqs, dtype=np.float64)
@@ -70,6 +74,9 @@ class DMSweep(object):
         self.D, self.C = self.table.shape
         self.max_bin = int(self.table.max()) if self.table.size else 0
         self.dtype = dtype
+        self.input_max = None if input_max is None else int(input_max)
+        if self.input_max is not None:
+            assert dtype in ("u8", "u16") and 1 <= self.input_max <= (255 if dtype == "u8" else 1023)
         self._plans = {}
 
     def _plan(self, code):
@@ -82,6 +89,9 @@ class DMSweep(object):
                 "pdd_sweep_plan_create")
             p = h
             self._plans[code] = p
+            if self.input_max is not None and code != _lib.F32:
+                _lib.check(_lib.lib().pdd_sweep_plan_set_input_max(p, self.input_max),
+                           "pdd_sweep_plan_set_input_max")
         return p
 
     def info(self, code=_lib.F32):
@@ -149,6 +159,9 @@ class DMSweep(object):
         elif x.dtype in _U16_TYPES:
             code = _lib.U16
             mode, pv = _pads16(x, self.C, padval)
+            if self.input_max is not None and mode == _lib.PAD_VALUE and float(padval) > self.input_max:
+                raise ValueError("pad %g above the sweep's input bound %d" % (float(padval),
+                                                                             self.input_max))
         elif x.dtype == torch.float32:
             code = _lib.F32
             mode, pv = _pad_args(x, padval)

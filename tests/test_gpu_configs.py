@@ -127,6 +127,97 @@ def test_config3_sweep_oracle_rows(gpu):
     ds.close()
 
 
+def test_config1_full_size_f32(gpu):
+    """BASELINE configs[1] at its full size -- 1024 ch x 2^20 samples x 1024
+    DMs (0-1000), float32: on integer data the float32 plane equals the exact
+    8-bit (u16-image) plane bit for bit, and sampled rows equal the fused
+    single-DM kernel (Spectra.dedispersed_series) and the oracle."""
+    import torch
+    from oracle import spectra_oracle as orc
+    from pypulsar_amd.formats.spectra import Spectra
+    from pypulsar_amd.sweep import DMSweep
+    C, N, D = 1024, 1 << 20, 1024
+    freqs = band(C)
+    dms = np.linspace(0.0, 1000.0, D)
+    x = _u8(C, N, 31)
+    x8 = torch.from_numpy(x).cuda()
+    xf = x8.float()
+    swf = DMSweep(dms, freqs, DT, dtype="f32")
+    pf = swf(xf)
+    assert pf.shape == (D, 1034083)
+    sw8 = DMSweep(dms, freqs, DT, dtype="u8")
+    assert torch.equal(sw8(x8), pf)
+    s = Spectra._from_device(freqs, DT, xf)
+    rows = [0, 511, 1023]
+    for d in rows:
+        assert torch.equal(s.dedispersed_series(dms[d], padval=0, trim=True)[:pf.shape[1]], pf[d])
+    want = orc.sweep_rows_inside(x, swf.table[rows], pf.shape[1])
+    np.testing.assert_array_equal(pf[rows].cpu().numpy().astype(np.float64), want)
+    swf.close()
+    sw8.close()
+
+
+def test_config1_fractional_f32_rows(gpu):
+    """configs[1] grid (1024 ch, 1024 DMs 0-1000) on genuinely fractional
+    float32 data (N = 2^17): sampled rows within 1e-5 relative of the
+    float64 oracle -- the north_star bar at the config's full 1024-channel
+    accumulation depth."""
+    import torch
+    from oracle import spectra_oracle as orc
+    from pypulsar_amd.sweep import DMSweep
+    C, N, D = 1024, 1 << 17, 1024
+    freqs = band(C)
+    dms = np.linspace(0.0, 1000.0, D)
+    rng = np.random.default_rng(41)
+    x = (rng.normal(0.0, 1.0, (C, N)) * 17.3 + 3.1).astype(np.float32)
+    sw = DMSweep(dms, freqs, DT, dtype="f32")
+    plane = sw(torch.from_numpy(x).cuda())
+    rows = [0, 1, 300, 777, 1022, 1023]
+    want = orc.sweep_rows_inside(x.astype(np.float64), sw.table[rows], plane.shape[1])
+    got = plane[rows].cpu().numpy()
+    for i, d in enumerate(rows):
+        assert rel_err(got[i], want[i]) <= 1e-5, "row %d" % d
+    sw.close()
+
+
+def test_config3_rehearsal_8_ranks(gpu):
+    """The 8-rank DM-sharded configs[3] step rehearsed on one GPU (VERDICT r2
+    #1): rank r = DMShardedSweep(world=8, rank=r) -- its own slice of each of
+    4 time batches corner-turned into the pieces block (P = N/32, a power of
+    two), its work-balanced DM slice (DDplan2b.py:272-273) swept from the
+    pieces at the GLOBAL trimmed width.  The 8 rank planes stacked equal the
+    one-shot plane bit for bit, and sampled rows equal the oracle."""
+    import torch
+    from oracle import spectra_oracle as orc
+    from pypulsar_amd.sharding import DMShardedSweep, split_block, trial_work
+    from pypulsar_amd.sweep import DMSweep
+    C, N, D, W, NB = 4096, 1 << 18, 4096, 8, 4
+    freqs = band(C)
+    dms = np.linspace(0.0, 1000.0, D)
+    x = _u8(C, N, 21)
+    block = torch.from_numpy(np.ascontiguousarray(x.T)).cuda()   # file order [N, C]
+    sw = DMSweep(dms, freqs, DT, dtype="u8")
+    plane = sw(block.t().contiguous())
+    sw.close()
+    shared, lo_prev = None, 0
+    for r in range(W):
+        ds = DMShardedSweep(dms, freqs, DT, N, dtype=torch.uint8, n_batches=NB,
+                            work=trial_work(dms, 1), device="cuda", world=W, rank=r, x_buf=shared)
+        assert ds.pieces and ds.P == N // (NB * W) and ds.lo == lo_prev
+        if shared is None:
+            ds.prefill(block)
+            shared = ds.x
+        for _ in range(2):  # a second step reuses every buffer
+            ds(split_block(block, NB, W, r))
+        assert torch.equal(ds.plane(), plane[ds.lo:ds.hi]), "rank %d rows differ" % r
+        lo_prev = ds.hi
+        ds.close()
+    assert lo_prev == D
+    rows = [0, 511, 512, 2047, 3584, 4095]
+    want = orc.sweep_rows_inside(x, orc.sweep_table(dms, freqs, DT)[rows], plane.shape[1])
+    np.testing.assert_array_equal(plane[rows].cpu().numpy().astype(np.float64), want)
+
+
 def test_config3_full_length_properties(gpu):
     """4096 ch x 2^22 samples x 4096 DMs: properties that hold at any size.
     (a) the exact 8-bit (u16-image) plane equals the float32-image plane;
@@ -167,13 +258,15 @@ def test_config3_full_length_properties(gpu):
     sub.close()
 
 
-@pytest.mark.parametrize("zdm", ["int", "float"])
+@pytest.mark.parametrize("zdm", ["wrap", "int", "float"])
 def test_config4_stream_equals_one_shot(gpu, zdm):
     """configs[4]: 4096-ch 8-bit blocks of 2^18 spectra, zero-DM + downsample
     2 + 2048-DM sweep, streamed from pinned host memory == the one-shot
-    pipeline over the whole stream.  'int' (the default): the exact 16-bit
-    path, also checked bit for bit against the oracle on a window of rows;
-    'float': the float32 path."""
+    pipeline over the whole stream.  'wrap' (the default; the reference's
+    uint8 result, zero_dm_filter.py:30-39) and 'int': the exact 16-bit path
+    -- the stream's sweep converts every 128 (wrap, image <= 510) / 64 (int,
+    <= 1020) channels, the one-shot sweep every 64 -- also checked bit for
+    bit against the oracle on a window of rows; 'float': the float32 path."""
     import torch
     from pypulsar_amd import _lib
     from pypulsar_amd._lib import call, ptr, stream_ptr
@@ -186,17 +279,19 @@ def test_config4_stream_equals_one_shot(gpu, zdm):
     N = 3 * block + 100000
     x = np.random.default_rng(13).integers(0, 256, size=(N, C), dtype=np.uint8)
     st = StreamingSweep(dms, freqs, DT, block=block, downsamp=ds, zero_dm=zdm)
-    assert st.ov == 7252 * ds and st.exact == (zdm == "int")
+    assert st.ov == 7252 * ds and st.exact == (zdm != "float")
+    assert st.input_max == {"wrap": 510, "int": 1020, "float": None}[zdm]
     chunks = [torch.from_numpy(x[i:i + block]).pin_memory() for i in range(0, N, block)]
     parts = [p.clone() for _, p in st(chunks)]
     st.close()
     got = torch.cat(parts, dim=1)
     xd = torch.from_numpy(x).cuda()
-    if zdm == "int":
+    if zdm != "float":
+        off = 255 * ds if zdm == "int" else 0
         img = torch.empty((C, N // ds), dtype=torch.int16, device="cuda")
-        prologue(xd, N, C, ds, "int", img, 255 * ds)
+        prologue(xd, N, C, ds, zdm, img, off)
         sw = DMSweep(dms, freqs, DT * ds, dtype="u16")
-        want = sw(img, out_bias=-255.0 * ds * C)
+        want = sw(img, out_bias=-float(off * C))
     else:
         f32 = torch.empty((C, N // ds), dtype=torch.float32, device="cuda")
         call("pdd_zdm_downsample", ptr(xd), _lib.U8, N, C, C, ds, 1, ptr(f32), f32.stride(0),
@@ -205,13 +300,13 @@ def test_config4_stream_equals_one_shot(gpu, zdm):
         want = sw(f32)
     assert got.shape == want.shape
     assert torch.equal(got, want)
-    if zdm == "int":
+    if zdm != "float":
         # oracle window: plane columns [j0, j0 + W) need input spectra
         # [j0 ds, (j0 + W + max_bin) ds) -- across the seam of blocks 1 and 2
         W, mb = 2048, sw.max_bin
         j0 = block // ds - 1000
         win = x[j0 * ds:(j0 + W + mb) * ds]
-        ref_img = orc.zdm_int_downsample(win, ds, "int")
+        ref_img = orc.zdm_int_downsample(win, ds, zdm)
         rows = [0, 1, 777, 1500, 2047]
         ref = orc.sweep_rows_inside(ref_img, sw.table[rows], W)
         np.testing.assert_array_equal(got[rows, j0:j0 + W].cpu().numpy(), ref)

@@ -190,3 +190,44 @@ def test_timeblock_ranges_cover():
     assert r[0][0] == 0 and r[-1][1] == 1000
     assert all(b[2] - a[2] == a[1] - a[0] for a, b in zip(r, r[1:]))
     assert all(x[3] - x[1] == 37 for x in r)
+
+
+@pytest.mark.parametrize("world,nbk,pieces", [(3, 2400, False), (4, 4096, True), (8, 4096, True)])
+def test_rehearsal_ranks_stack_to_one_shot(world, nbk, pieces):
+    """DMShardedSweep(world=W, rank=r) on one process: every rank's exact
+    compute (own slice's corner turn, DM slice at the global width, batch by
+    batch) over a shared pre-filled block; the W rank planes stacked are the
+    one-shot plane (host logic of bench.py --rehearse; the GPU test runs the
+    HIP kernels at the configs[3] geometry)."""
+    from oracle import spectra_oracle as orc
+    C = 16
+    freqs = _band(C)
+    dms = np.linspace(0.0, 40.0, 11)
+    work = np.r_[np.ones(5), np.full(len(dms) - 5, 0.5)]
+    tab = orc.sweep_table(dms, freqs, DT)
+
+    def to_cm(src_tc, dst_cm):
+        dst_cm.copy_(src_tc.t())
+
+    def sweep_fn(x, N, piece, x_off, sub, out, n_cols):
+        if piece:
+            x = x.reshape(N // piece, C, piece).permute(1, 0, 2).reshape(C, N)
+        t = orc.sweep_table(sub, freqs, DT)
+        xv = x[:, x_off:x_off + n_cols + int(t.max())]
+        out.copy_(torch.from_numpy(orc.sweep_plane(xv.numpy().astype(np.float64), t,
+                                                   n_out=n_cols).astype(np.float32)))
+
+    block = torch.from_numpy(_data(C, nbk).T.copy())         # time-major [N, C]
+    shared, rows = None, []
+    for r in range(world):
+        ds = sharding.DMShardedSweep(dms, freqs, DT, nbk, dtype=torch.float32, n_batches=2,
+                                     work=work, to_cm=to_cm, sweep_fn=sweep_fn, world=world,
+                                     rank=r, x_buf=shared)
+        assert ds.pieces == pieces and ds.world == world and ds.rank == r
+        if shared is None:
+            ds.prefill(block)
+            shared = ds.x
+        ds(sharding.split_block(block, 2, world, r))
+        rows.append(ds.plane().numpy())
+    want = orc.sweep_plane(_data(C, nbk).astype(np.float64), tab)
+    np.testing.assert_array_equal(np.concatenate(rows).astype(np.float64), want)
