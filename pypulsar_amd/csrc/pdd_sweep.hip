@@ -1300,7 +1300,9 @@ static int64_t il_seg_samples(const pdd_sweep_plan* p) {
   const int Tq = 64 * p->v.G;
   const int64_t C = p->C * p->n_grp;
   const int64_t lo = std::min(0, p->min_bin), hi = std::max(0, p->max_bin);
-  int64_t budget = (int64_t)8 << 30;  // bytes of R per segment
+  // bytes of R per segment: 16 GiB = one segment per quarter of a 4096 x
+  // 2^22 block (configs[3] at 4 time batches), few launches per step
+  int64_t budget = (int64_t)16 << 30;
   if (const char* e = getenv("PDD_SWEEP_SEG_BYTES")) budget = std::max<int64_t>(atoll(e), 1 << 16);
   const int64_t nr_max = budget / (C * 16);
   return (nr_max - (hi - lo) - 64) / Tq * Tq * p->v.S;

@@ -68,3 +68,33 @@ def test_psrfits_then_dedisperse(gpu, tmp_path):
     got = s.data
     assert got.shape == want.shape
     assert np.max(np.abs(got - want)) <= 1e-5 * np.max(np.abs(want))
+
+
+@pytest.mark.parametrize("nbits", [4, 8, 16, 32])
+@pytest.mark.parametrize("order", ["asc", "desc"])
+def test_device_decode_matches_reference_fixtures(gpu, tmp_path, nbits, order):
+    """k_psrfits_subints (through PsrfitsFile.read_subint / get_spectra of a
+    file holding the fixture's subints) against the REFERENCE's own outputs
+    (tests/golden/golden_psrfits.npz, made by executing
+    /root/reference/formats/psrfits.py:37-183): bit-exact float32 values,
+    frequencies and start times (VERDICT r2 #6: f3 pinned)."""
+    import os
+    from pypulsar_amd.formats.psrfits import PsrfitsFile, write_search_psrfits
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_psrfits.npz"))
+    key = "b%d_%s" % (nbits, order)
+    fn = str(tmp_path / ("%s.fits" % key))
+    write_search_psrfits(fn, g[key + "_data"], g[key + "_freqs"], 64e-6, nbits, g[key + "_scl"],
+                         g[key + "_off"], g[key + "_wts"])
+    pf = PsrfitsFile(fn)
+    assert pf.specinfo.need_flipband == bool(g[key + "_flip"])
+    for isub in (0, 3):
+        np.testing.assert_array_equal(pf.read_subint(isub), g["%s_sub%d" % (key, isub)])
+    for k, (start, n) in enumerate(g["spans"]):
+        s = pf.get_spectra(int(start), int(n))
+        np.testing.assert_array_equal(s.device_data.cpu().numpy().astype(np.float64),
+                                      g["%s_span%d" % (key, k)])
+        np.testing.assert_array_equal(s.freqs, g["%s_span%d_freqs" % (key, k)])
+        assert s.starttime == float(g["%s_span%d_start" % (key, k)])
+    if nbits == 8:
+        got = pf.read_subint(1, apply_weights=False, apply_scales=True, apply_offsets=False)
+        np.testing.assert_array_equal(got, g[key + "_flags"])

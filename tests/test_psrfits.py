@@ -96,3 +96,69 @@ def test_not_psrfits(tmp_path):
     assert not is_PSRFITS(fn)
     with pytest.raises(ValueError):
         SpectraInfo([fn])
+
+
+GOLD = None
+
+
+def _gold():
+    global GOLD
+    if GOLD is None:
+        import os
+        GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_psrfits.npz"))
+    return GOLD
+
+
+def _stored(data, nbits):
+    flat = data.reshape(data.shape[0], -1)
+    if nbits == 4:
+        return ((flat[:, 0::2] & 15) | ((flat[:, 1::2] & 15) << 4)).astype(np.uint8)
+    return flat.astype({8: np.uint8, 16: ">i2", 32: ">f4"}[nbits])
+
+
+@pytest.mark.parametrize("nbits", [4, 8, 16, 32])
+@pytest.mark.parametrize("order", ["asc", "desc"])
+def test_oracle_matches_reference_fixtures(nbits, order):
+    """oracle/psrfits_oracle.py against the reference's own read_subint /
+    get_spectra outputs (tests/golden/make_golden_psrfits.py executed
+    /root/reference/formats/psrfits.py:37-183): bit-exact."""
+    g = _gold()
+    key = "b%d_%s" % (nbits, order)
+    nsub, nsblk, nchan = (int(v) for v in g["geom"])
+    data, freqs = g[key + "_data"], g[key + "_freqs"]
+    scl, off, wts = g[key + "_scl"], g[key + "_off"], g[key + "_wts"]
+    body = _stored(data, nbits)
+    subs = [po.read_subint(body[i], nbits, nsblk, nchan, scl[i].astype(">f4"),
+                           off[i].astype(">f4"), wts[i].astype(">f4")) for i in range(nsub)]
+    for isub in (0, 3):
+        np.testing.assert_array_equal(subs[isub], g["%s_sub%d" % (key, isub)])
+        assert subs[isub].dtype == g["%s_sub%d" % (key, isub)].dtype == np.float32
+    for k, (start, n) in enumerate(g["spans"]):
+        want = g["%s_span%d" % (key, k)]
+        got, gf = po.get_spectra(subs, nsblk, freqs, bool(g[key + "_flip"]), int(start), int(n))
+        np.testing.assert_array_equal(np.asarray(got, dtype=np.float64), want)
+        np.testing.assert_array_equal(gf, g["%s_span%d_freqs" % (key, k)])
+    if nbits == 8:
+        got = po.read_subint(body[1], 8, nsblk, nchan, scl[1], off[1], wts[1], apply_weights=False,
+                             apply_offsets=False)
+        np.testing.assert_array_equal(got, g[key + "_flags"])
+
+
+def test_unpack_4bit_reference_fixture():
+    from pypulsar_amd.formats.psrfits import unpack_4bit
+    g = _gold()
+    np.testing.assert_array_equal(unpack_4bit(g["unpack4_in"]), g["unpack4_out"])
+    np.testing.assert_array_equal(po.unpack_4bit(g["unpack4_in"]), g["unpack4_out"])
+
+
+@pytest.mark.parametrize("order", ["asc", "desc"])
+def test_spectrainfo_flipband_matches_reference_case(tmp_path, order):
+    """The header this repo's writer produces for the fixture band gives the
+    need_flipband the reference case used (psrfits.py:459-464)."""
+    from pypulsar_amd.formats.psrfits import SpectraInfo, write_search_psrfits
+    g = _gold()
+    key = "b8_%s" % order
+    fn = str(tmp_path / "f.fits")
+    write_search_psrfits(fn, g[key + "_data"], g[key + "_freqs"], 64e-6, 8, g[key + "_scl"],
+                         g[key + "_off"], g[key + "_wts"])
+    assert SpectraInfo([fn]).need_flipband == bool(g[key + "_flip"])
