@@ -885,6 +885,9 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       for (int i = 0; i < NBUF - 2; ++i) younger += hist[i];
       wait_vmcnt(younger);
       if (stamps) { tB = __builtin_amdgcn_s_memtime(); ts_wait += tB - tA; tA = tB; }
+#ifdef PDD_SWEEP_DEV
+      if (!(dbg & 64))  // dbg bit 6 (timing only, wrong results): no chunk barriers
+#endif
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (stamps) { tB = __builtin_amdgcn_s_memtime(); ts_poll += tB - tA; tA = tB; }
@@ -958,6 +961,9 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       tA = __builtin_amdgcn_s_memtime();
       ts_comp += tA - tB;
     }
+#ifdef PDD_SWEEP_DEV
+    if (!(dbg & 64))
+#endif
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (stamps) { tB = __builtin_amdgcn_s_memtime(); ts_poll += tB - tA; }
@@ -973,8 +979,11 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     typedef __attribute__((address_space(3))) int lds_int_t;
     const int ml = min(lane / DPW, CC - 1) * ROW + lane % DPW;
     const int vmeta = *(const lds_int_t*)(uintptr_t)(meta_base + (uint32_t)((slot * SLOT + ml) * 4));
-    const int ncc = __builtin_amdgcn_readfirstlane(*(const lds_int_t*)(uintptr_t)(
+    int ncc = __builtin_amdgcn_readfirstlane(*(const lds_int_t*)(uintptr_t)(
         lds_addr_of(metar) + (uint32_t)((slot * SLOT + DB + 3) * 4))) >> 20;
+#ifdef PDD_SWEEP_DEV
+    if (dbg & 64) ncc = cht_t[1 + k] >> 20;  // no barrier: the ring may not hold chunk k yet
+#endif
     auto chan_base = [&](int) -> uint32_t { return lane_byte + (uint32_t)(b * buf_e * 16); };
     if (!(dbg & 2)) {
       if constexpr (U16) {
