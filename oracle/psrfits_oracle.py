@@ -6,10 +6,14 @@ arrays a test wrote (not on the product's FITS reader):
   read_subint   formats/psrfits.py:67-107  ((data*scales)+offsets)*weights
   get_spectra   formats/psrfits.py:140-183 (concatenate, transpose, skip/trunc,
                 flip the band when it ascends)
-No PSRFITS file ships with the reference, so parity with real files is
-unpinned; the restatement follows the reference lines above exactly,
+Pinned: tests/test_psrfits.py checks every function here against
+tests/golden/golden_psrfits.npz, the outputs of the reference's own
+formats/psrfits.py executed in the build container
+(tests/golden/make_golden_psrfits.py): bit-exact for 4/8/16/32-bit data and
+both band orders.  The restatement follows the reference lines above,
 including numpy's float32 promotion of uint8/int16 data times float32
-scales.
+scales.  No PSRFITS file from a real backend ships with the reference, so
+parity with such files is unpinned.
 """
 import numpy as np
 
