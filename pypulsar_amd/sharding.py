@@ -153,6 +153,12 @@ class DMShardedSweep(object):
     by the CPU tests; the defaults are pdd_corner_turn and the HIP DMSweep of
     this rank's slice (built once).
 
+    ``gather_fn(out, cm, k)`` (pieces layout) replaces the async RCCL
+    all-gather of batch k -- ``out`` = the batch's [W*C, P] pieces, ``cm`` =
+    this rank's corner-turned slice -- and returns an object with ``wait()``
+    (the GPU test injects a delayed loopback on a side stream to check the
+    pipeline's stream ordering with real HIP kernels).
+
     Rehearsal (``world=W, rank=r`` given; no process group needed): the
     exact compute of rank r of a W-rank run -- its own slice's corner turn
     into the block, its DM slice swept at the global width, batch by batch
@@ -164,7 +170,7 @@ class DMShardedSweep(object):
 
     def __init__(self, dms, freqs, dt, N, dtype=torch.uint8, n_batches=1, work=None,
                  gather=False, dst=0, group=None, device=None, to_cm=None, sweep_fn=None,
-                 pieces=None, world=None, rank=None, x_buf=None):
+                 pieces=None, world=None, rank=None, x_buf=None, gather_fn=None):
         from . import delays as _delays
         self.group = group
         self.rehearse = world is not None
@@ -214,10 +220,13 @@ class DMShardedSweep(object):
             self.x = x_buf
         else:
             self.x = torch.empty(xshape, dtype=dtype, device=self.device)
+        self.gather_fn = gather_fn
+        assert gather_fn is None or self.pieces, "gather_fn takes the pieces layout"
+        self.direct = self.rehearse and gather_fn is None  # rehearsal writes its piece in place
         if self.pieces:
             # two corner-turn buffers: batch k+1's turn must not overwrite the
             # one batch k's all-gather may still be reading
-            self.cm = ([] if self.rehearse else
+            self.cm = ([] if self.direct else
                        [torch.empty((self.C, self.P), dtype=dtype, device=self.device)
                         for _ in range(2)])
             self.xt = None
@@ -274,7 +283,7 @@ class DMShardedSweep(object):
         """Batch k into x: this rank's corner turn (+ the async all-gather of
         every rank's slice); returns the pending collective or None."""
         W, T, P = self.world, self.T, self.P
-        if self.rehearse:
+        if self.direct:
             # this rank's own slice only; the others' are already in x
             r = self.rank
             if self.pieces:
@@ -289,6 +298,8 @@ class DMShardedSweep(object):
                 return None
             cm = self.cm[k % 2]
             self.to_cm(part[k], cm)
+            if self.gather_fn is not None:
+                return self.gather_fn(dst.view(W * self.C, P), cm, k)
             return _all_gather_into(dst.view(W * self.C, P), cm, group=self.group,
                                     async_op=True)
         if W == 1:
