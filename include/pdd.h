@@ -176,6 +176,22 @@ typedef struct pdd_sweep_plan pdd_sweep_plan;
  * <= 1023) input. */
 int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int dtype,
                           pdd_sweep_plan** plan);
+/* The same with plan flags (pdd_sweep_plan_create = PDD_SWEEP_FACTOR):
+ * PDD_SWEEP_FACTOR lets an 8-bit plan (C a multiple of 4) sweep EXACTLY
+ * factorised over groups of 4 adjacent channels when that pays: each
+ * group's distinct relative-shift patterns are summed once (stage 1), and
+ * every trial adds its pattern series at the group's base shift (stage 2) --
+ * the same integer samples as the channel-by-channel sum, so the plane is
+ * bit-identical; flags 0 forces the channel-by-channel kernel. */
+#define PDD_SWEEP_FACTOR 1
+/* with PDD_SWEEP_FACTOR: factorise whenever the windows fit, paying or not
+ * (tests of small grids) */
+#define PDD_SWEEP_FACTOR_FORCE 2
+int pdd_sweep_plan_create_ex(const int32_t* host_table, int64_t D, int64_t C, int dtype, int flags,
+                             pdd_sweep_plan** plan);
+/* Channels per factor group of the plan (0 = channel by channel) and, if
+ * n_patterns is non-null, its stage-1 pattern count. */
+int pdd_sweep_plan_factor(const pdd_sweep_plan* plan, int64_t* n_patterns);
 /* x: [C][N] (ld) of the plan's dtype; out: [D][ld_out] float32.
  * For PDD_U8 with PDD_PAD_VALUE every padvals[c] must be an integer in
  * [0, 255] (checked on the host side by the caller).  PDD_U16 input: unsigned

@@ -25,6 +25,8 @@ STAT_MEAN, STAT_MEDIAN, STAT_STD, STAT_MIN, STAT_MAX = 0, 1, 2, 3, 4
 LAYOUT_TIME_MAJOR, LAYOUT_CHAN_MAJOR = 0, 1
 ENOCHAIN = -5          # pdd_subband_chain: geometry does not chain (nothing launched)
 ZDM_NONE, ZDM_INT, ZDM_WRAP = 0, 1, 2
+SWEEP_FACTOR = 1       # pdd_sweep_plan_create_ex: exact factorised 8-bit sweeps allowed
+SWEEP_FACTOR_FORCE = 2  # ... and taken whenever the windows fit (tests)
 
 # every symbol include/pdd.h declares (checked by tests/test_abi.py)
 EXPORTS = (
@@ -38,6 +40,7 @@ EXPORTS = (
     "pdd_sp_search", "pdd_psrfits_subints", "pdd_downsample_u8", "pdd_sweep_timing_read",
     "pdd_sweep_execute_ex", "pdd_zdm_int_downsample", "pdd_downsample_u8_u16",
     "pdd_sweep_execute_ds", "pdd_subband_chain", "pdd_scratch_release",
+    "pdd_sweep_plan_create_ex", "pdd_sweep_plan_factor",
 )
 
 
@@ -68,6 +71,8 @@ _SIGS = {
     "pdd_downsample_u8_u16": ([_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp], _int),
     "pdd_zero_dm": ([_vp, _int, _i64, _i64, _i64, _int, _vp, _i64, _vp], _int),
     "pdd_sweep_plan_create": ([_vp, _i64, _i64, _int, ctypes.POINTER(_vp)], _int),
+    "pdd_sweep_plan_create_ex": ([_vp, _i64, _i64, _int, _int, ctypes.POINTER(_vp)], _int),
+    "pdd_sweep_plan_factor": ([_vp, _vp], _int),
     "pdd_sweep_execute": ([_vp, _vp, _i64, _i64, _int, _vp, _vp, _i64, _i64, _vp], _int),
     "pdd_sweep_execute_ex": ([_vp, _vp, _i64, _i64, _i64, _i64, _int, _vp, _vp, _i64, _i64,
                               ctypes.c_float, _vp], _int),

@@ -52,7 +52,7 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // synchronisation, were seen to alias live hipMalloc buffers -- wrong sweep
 // results in tests/native/abi_asan.cpp.)  Returns nullptr and sets the error
 // message on failure.
-enum { kScratchImage = 0, kScratchChain = 1, kScratchPartial = 2, kScratchSmall = 3 };
+enum { kScratchImage = 0, kScratchChain = 1, kScratchPartial = 2, kScratchSmall = 3, kScratchPattern = 4 };
 void* scratch(hipStream_t st, int slot, size_t bytes);
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

@@ -25,9 +25,11 @@
 //  * blockIdx is remapped so the n_dblk DM blocks of one time tile run
 //    back to back on ONE XCD and re-read the tile's input from that XCD's L2.
 #include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
+#include <unordered_map>
 #include <utility>
 #include <vector>
 
@@ -639,6 +641,50 @@ __global__ __launch_bounds__(256) void k_interleave_u16_ds_v(const uint8_t* __re
                           v[4][e] | (v[5][e] << 16), v[6][e] | (v[7][e] << 16));
 }
 
+// ------------------------------------------------------------------ factorised sweep
+// Exact factorisation of the 8-bit sweep over groups of FX = 4 adjacent
+// channels.  Within a group (channels c0..c0+3) trial d's shifts are its base
+// shift b = table[d][c0] plus a RELATIVE pattern r = (0, r1, r2, r3); the
+// group's contribution to plane[d][t] is
+//     sum_k X(c0 + k, t + b + r_k) = S_r(t + b),  S_r(u) = sum_k X(c0 + k, u + r_k),
+// the same samples summed in integers, so the plane is bit-identical to the
+// channel-by-channel sum.  Across a DM grid a group takes few distinct
+// patterns (configs[3]: 27 769 over 1024 groups, 6.8 per group): stage 1
+// (k_fx_patterns) writes every pattern series S_r once as a u16-eighths image
+// row (sums of four samples <= 1020 stay exact in the packed u16 lanes), and
+// stage 2 is k_sweep_il over the GROUPS, each trial reading its pattern's
+// window at its base shift: a quarter of the LDS reads and adds of the
+// channel sweep, the same window staging (a tile stages every pattern its
+// trials use: 3.8 of a group's patterns per 48-trial block, 0.88 x the
+// channel windows' elements).
+constexpr int kFx = 4;
+__global__ __launch_bounds__(256) void k_fx_patterns(const uint4* __restrict__ R, int64_t nR,
+                                                     const int4* __restrict__ pat,
+                                                     uint4* __restrict__ P) {
+  const int64_t p = blockIdx.x;
+  const int4 q = pat[p];  // {c0, r1, r2, r3}
+  const uint4* r0 = R + (int64_t)q.x * nR;
+  const int64_t j0 = (int64_t)blockIdx.y * (256 * kIlPer) + threadIdx.x;
+  auto at = [&](int k, int r, int64_t j) -> uint4 {
+    const int64_t e = j + r;  // elements no trial reads may fall outside the row
+    return (e >= 0 && e < nR) ? r0[(int64_t)k * nR + e] : make_uint4(0u, 0u, 0u, 0u);
+  };
+  uint4 v[kIlPer];
+#pragma unroll
+  for (int i = 0; i < kIlPer; ++i) {
+    const int64_t j = j0 + i * 256;
+    if (j >= nR) continue;
+    const uint4 a = at(0, 0, j), b = at(1, q.y, j), c = at(2, q.z, j), d = at(3, q.w, j);
+    v[i] = make_uint4(a.x + b.x + c.x + d.x, a.y + b.y + c.y + d.y, a.z + b.z + c.z + d.z,
+                      a.w + b.w + c.w + d.w);
+  }
+#pragma unroll
+  for (int i = 0; i < kIlPer; ++i) {
+    const int64_t j = j0 + i * 256;
+    if (j < nR) P[p * nR + j] = v[i];
+  }
+}
+
 // n DMAs of 64 elements (1 KiB) each, q = first, first + step, ...
 __device__ __forceinline__ int stage_il_dma(uint32_t lds_dst, const float4* src, int ne, int first,
                                             int step, int lane) {
@@ -766,13 +812,19 @@ __device__ __forceinline__ uint32_t add3_u32(uint32_t a, uint32_t b, uint32_t c)
   return a + b + c;
 }
 
-template <int G, int DPW, int NCW, int NLW, int CC, int NBUF, bool U16 = false>
+// Factorised sweeps (FX): the kernel's "channels" are the channel groups;
+// a chunk's windows (one per pattern its trials use) come from the plan's
+// window records wt[dblk][chunk][kFxWin] = {bmin, length, buffer offset,
+// pattern row | window count << 20}, read by one vector load per loader lane
+// an iteration ahead.
+constexpr int kFxWin = 64;
+template <int G, int DPW, int NCW, int NLW, int CC, int NBUF, bool U16 = false, bool FX = false>
 __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const float4* __restrict__ R0, int64_t nR, int C, int lo, const int* __restrict__ mt,
     const int* __restrict__ cht, int maxch, float* __restrict__ out, int64_t ld_out, int D,
     int64_t Qs, int64_t t_base, int64_t n_out, int buf_e, int n_tblk, int n_dblk, int dbg,
     int64_t row_g, int64_t row_d, int flush_n, float out_bias, const float* __restrict__ r2_pad,
-    int64_t r2_nR, int64_t r2_ov) {
+    int64_t r2_nR, int64_t r2_ov, const int4* __restrict__ wt) {
   // Grouped sweeps: C is the channel count of ONE group; blockIdx.x / (tiles
   // per group) is the group, whose channels are R rows [grp*C, grp*C + C),
   // whose tables are mt[grp][...], and whose trial d lands in plane row
@@ -783,6 +835,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   constexpr int SLOT = il_slot(CC, DB);
   constexpr int MA = il_ma(NBUF), MR = il_mr(NBUF);
   constexpr int S = U16 ? 8 : 4;  // samples per 16-byte element (quarters / eighths)
+  static_assert(!FX || U16, "factorised sweeps run on the u16 eighths");
   static_assert(DPW == 4 && G == (U16 ? 2 : 4) && DPW * CC <= 64 && CC % 2 == 0,
                 "4 trials per wave, 4 (f32) or 2 (u16) groups; one lane per (channel, trial)");
   static_assert(NBUF >= 2 && MA >= 2 * NBUF - 2 && MR > MA, "ring geometry");
@@ -839,8 +892,37 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       }
       return n;
     };
+    // FX: the chunk's window records, lane i = window i (vector load)
+    const int4* wt_b = FX ? wt + ((int64_t)grp * n_dblk + dblk) * maxch * kFxWin : nullptr;
+    auto load_rec = [&](int k) -> int4 {
+      if constexpr (FX) return wt_b[(int64_t)min(k, nchunk - 1) * kFxWin + lane];
+      else return make_int4(0, 0, 0, 0);
+    };
+    int4 rec_next = load_rec(0);
     auto issue_samples = [&](int k) -> int {
       if (dbg & 1) return 0;
+      if constexpr (FX) {
+        // the record of chunk k was loaded an iteration ahead (the wait for
+        // it is the one this iteration already did); load chunk k + 1's now
+        const int4 rec = rec_next;
+        asm volatile("" ::"v"(rec.x), "v"(rec.y), "v"(rec.z), "v"(rec.w));
+        const int b = k % NBUF;
+        const int nw = __builtin_amdgcn_readlane(rec.w, 0) >> 20;
+        int n = 0;
+        for (int i = 0; i < nw; ++i) {
+          const int bm = __builtin_amdgcn_readlane(rec.x, i);
+          const int len = __builtin_amdgcn_readlane(rec.y, i);
+          const int off = __builtin_amdgcn_readlane(rec.z, i);
+          const int row = __builtin_amdgcn_readlane(rec.w, i) & 0xfffff;
+          n += stage_il_dma(img_lds + (uint32_t)((b * buf_e + off) * 16),
+                            R + (int64_t)row * nR + (t0 + bm - lo), len, lw, NLW, lane);
+        }
+        if (k + 1 < nchunk) {
+          rec_next = load_rec(k + 1);
+          ++n;  // rides on the counted vmcnt
+        }
+        return n;
+      }
       const int b = k % NBUF;
       // the chunk's window rows {bmin, span, offset, source row} by scalar
       // loads from the global table, all eight issued before one wait: the
@@ -891,7 +973,10 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (stamps) { tB = __builtin_amdgcn_s_memtime(); ts_poll += tB - tA; tA = tB; }
-      const int n = issue_meta(k + MA) + (k + NBUF - 1 < nchunk ? issue_samples(k + NBUF - 1) : 0);
+      // samples first: in FX tiles the compiler's wait for the window
+      // records (it cannot see the DMAs) lands before any DMA of this iteration
+      int n = k + NBUF - 1 < nchunk ? issue_samples(k + NBUF - 1) : 0;
+      n += issue_meta(k + MA);
 #pragma unroll
       for (int i = NBUF - 1; i > 0; --i) hist[i] = hist[i - 1];
       hist[0] = n;
@@ -1194,8 +1279,13 @@ static constexpr int kLdsMax = 160 * 1024;
 
 typedef void (*sweep_il_fn)(const float4*, int64_t, int, int, const int*, const int*, int, float*,
                             int64_t, int, int64_t, int64_t, int64_t, int, int, int, int, int64_t,
-                            int64_t, int, float, const float*, int64_t, int64_t);
-static sweep_il_fn il_kernel_for(const Variant& v) {
+                            int64_t, int, float, const float*, int64_t, int64_t, const int4*);
+static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false) {
+  if (fx) {
+    if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
+      return k_sweep_il<2, 4, 12, 4, 8, 2, true, true>;
+    return nullptr;
+  }
 #define IL(NCW_, NLW_, CC_, NB_)                                                              \
   if (v.S == 4 && v.NW == NCW_ && v.NLW == NLW_ && v.CC == CC_ && v.NBUF == NB_ && v.G == 4 && \
       v.DPW == 4)                                                                               \
@@ -1281,6 +1371,11 @@ struct pdd_sweep_plan {
   uint16_t* d_win = nullptr;
   uint8_t* d_rows = nullptr;
   int rows_max = 0, nchunk = 0;
+  int fx = 0;              // factorised sweep: channels per group (0 = channel by channel)
+  int64_t n_pat = 0;       // factorised: pattern series (stage-1 rows, + 1 zero row)
+  int64_t fx_rows = 0;     // factorised: metadata rows per trial block (groups + pad groups)
+  int* d_pat = nullptr;    // factorised: [n_pat][4] {c0, r1, r2, r3}
+  int* d_wt = nullptr;     // factorised: [n_dblk][maxch][kFxWin][4] window records
   int dtype = PDD_F32;     // input element type
   int input_max = 0;       // largest input value (integer input; 0 = the dtype's bound)
   int64_t n_grp = 1;       // independent channel groups (grouped sweep)
@@ -1317,8 +1412,11 @@ static int64_t il_seg_samples(const pdd_sweep_plan* p) {
   // bytes of R per segment: 16 GiB = one segment per quarter of a 4096 x
   // 2^22 block (configs[3] at 4 time batches), few launches per step
   int64_t budget = (int64_t)16 << 30;
+  // factorised plans also hold the stage-1 pattern image (n_pat + 1 rows)
+  const int64_t rows = C + (p->fx ? p->n_pat + 2 : 0);
+  if (p->fx) budget = (int64_t)40 << 30;
   if (const char* e = getenv("PDD_SWEEP_SEG_BYTES")) budget = std::max<int64_t>(atoll(e), 1 << 16);
-  const int64_t nr_max = budget / (C * 16);
+  const int64_t nr_max = budget / (rows * 16);
   return (nr_max - (hi - lo) - 64) / Tq * Tq * p->v.S;
 }
 
@@ -1342,7 +1440,8 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
   // of 8-bit values, 64 of 16-bit values <= 1023, 128 of the wrap-mode
   // zero-DM image downsampled by 2 (<= 510; pdd_sweep_plan_set_input_max)
   const int vmax = p->input_max > 0 ? p->input_max : (p->dtype == PDD_U8 ? 255 : 1023);
-  const int flush_n = std::min(256, 65535 / vmax);
+  // (factorised: the swept pattern series are sums of fx samples)
+  const int flush_n = std::min(256, 65535 / (vmax * std::max(1, p->fx)));
   const int64_t C = p->C * p->n_grp;  // all channels (groups are contiguous channel ranges)
   const int64_t lo = std::min(0, p->min_bin), hi = std::max(0, p->max_bin);
   int64_t seg = il_seg_samples(p);  // output samples per segment
@@ -1366,6 +1465,14 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
   if (!ex.R_pre) {
     R = static_cast<float4*>(scratch(st, kScratchImage, (size_t)((C + 1) * nr_alloc) * sizeof(float4)));
     if (!R) return -2;
+  }
+  // factorised plans: the pattern image (stage 1), n_pat rows + a row of zeros
+  uint4* P = nullptr;
+  if (p->fx) {
+    PDD_REQUIRE(u16 && p->dtype == PDD_U8 && ds == 1 && !ex.r2_pad && !ex.R_pre && p->n_grp == 1,
+                "pdd_sweep_execute: factorised plans take 8-bit input at the raw rate");
+    P = static_cast<uint4*>(scratch(st, kScratchPattern, (size_t)((p->n_pat + 1) * nr_alloc) * sizeof(uint4)));
+    if (!P) return -2;
   }
   const int dbg = debug_flags();
   int rc = 0;
@@ -1418,6 +1525,15 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
       hipLaunchKernelGGL(k_interleave<float>, g1, dim3(256), 0, st, (const float*)x, lay, N,
                          t_base + lo + x_off, Qs, nR, pad_mode, padvals, R);
     if (hipGetLastError() != hipSuccess) { rc = -3; break; }
+    if (p->fx) {
+      if (hipMemsetAsync(P + p->n_pat * nR, 0, (size_t)nR * sizeof(uint4), st) != hipSuccess) {
+        rc = -3;
+        break;
+      }
+      hipLaunchKernelGGL(k_fx_patterns, dim3((unsigned)p->n_pat, (unsigned)cdiv(nR, 256 * kIlPer)),
+                         dim3(256), 0, st, (const uint4*)R, nR, (const int4*)p->d_pat, P);
+      if (hipGetLastError() != hipSuccess) { rc = -3; break; }
+    }
     const int64_t n_tblk = Qs / Tq;
     const int64_t blocks = n_tblk * p->n_dblk * p->n_grp;
     if (blocks >= (1ll << 31)) { rc = -1; break; }
@@ -1425,11 +1541,12 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
     const bool bracket = p->timing && p->timed < pdd_sweep_plan::kEvPairs;
     if (p->timing && !bracket) pm->dropped++;
     if (bracket) (void)hipEventRecord(p->ev[2 * p->timed], st);
-    hipLaunchKernelGGL(il_kernel_for(p->v), dim3((unsigned)blocks), dim3(p->v.threads()),
-                       p->lds_bytes, st, ex.R_pre ? ex.R_pre : R, nR, (int)p->C, (int)lo, p->d_tab,
+    hipLaunchKernelGGL(il_kernel_for(p->v, p->fx != 0), dim3((unsigned)blocks), dim3(p->v.threads()),
+                       p->lds_bytes, st, ex.R_pre ? ex.R_pre : (p->fx ? (const float4*)P : R), nR,
+                       (int)(p->fx ? p->fx_rows - 1 : p->C), (int)lo, p->d_tab,
                        p->d_bmin, p->maxch, out, ld_out, (int)p->D, Qs, t_base, t_base + cnt,
                        p->stride, (int)n_tblk, (int)p->n_dblk, dbg, row_g, row_d, flush_n, out_bias,
-                       ex.r2_pad, ex.r2_nR, ex.r2_ov);
+                       ex.r2_pad, ex.r2_nR, ex.r2_ov, (const int4*)p->d_wt);
     if (hipGetLastError() != hipSuccess) rc = -3;
     if (bracket) {
       (void)hipEventRecord(p->ev[2 * p->timed + 1], st);
@@ -1444,13 +1561,198 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
 
 extern "C" {
 
+// Tables of a factorised plan (module comment at k_fx_patterns): the
+// pattern pool, the per-(trial block, group) metadata rows in the layout of
+// the channel sweep (DB LDS byte offsets -- the trial's pattern window +
+// base shift -- then {0, 0, 0, group | groups in the chunk << 20}), the chunk
+// tables, and the window records of every chunk.  Returns false when a chunk
+// cannot hold a group pair's windows or the factorisation does not pay.
+struct FxTables {
+  std::vector<int> pat, mt, cht, wt;
+  int64_t n_pat = 0, rows_pb = 0;  // metadata rows per trial block
+  int maxch = 0;
+};
+static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v, int64_t buf_e,
+                     bool force, FxTables& T) {
+  if (C % kFx != 0 || C < 2 * kFx) return false;
+  const int64_t NG = C / kFx, DB = v.DB(), ROW = DB + 4, Tq = 64 * v.G;
+  const int64_t n_dblk = cdiv(D, DB);
+  // pattern of (trial, group): relative shifts r1..r3 (packed key) -> pool row
+  std::vector<int> pid((size_t)(D * NG));
+  std::unordered_map<uint64_t, int> idx;
+  T.pat.clear();
+  for (int64_t g = 0; g < NG; ++g) {
+    idx.clear();
+    for (int64_t d = 0; d < D; ++d) {
+      const int32_t* r = tab + d * C + g * kFx;
+      uint64_t key = 0;
+      for (int k = 1; k < kFx; ++k) {
+        const int64_t rel = (int64_t)r[k] - r[0];
+        if (rel < -(1 << 20) || rel >= (1 << 20)) return false;
+        key = (key << 21) | (uint64_t)(rel + (1 << 20));
+      }
+      auto it = idx.find(key);
+      int id;
+      if (it == idx.end()) {
+        id = (int)(T.pat.size() / 4);
+        idx.emplace(key, id);
+        T.pat.push_back((int)(g * kFx));
+        for (int k = 1; k < kFx; ++k) T.pat.push_back(r[k] - r[0]);
+      } else {
+        id = it->second;
+      }
+      pid[(size_t)(d * NG + g)] = id;
+    }
+  }
+  T.n_pat = (int64_t)T.pat.size() / 4;
+  // pays when stage 1 (4 adds per pattern sample) + stage 2 (one add per
+  // trial and group) is at most half of the channel sweep's adds
+  if (!force && (double)T.n_pat * kFx + (double)D * NG > 0.5 * (double)D * C) return false;
+  if (T.n_pat + 1 >= (1 << 20)) return false;
+  const int zero_row = (int)T.n_pat;  // pad groups read a window of this row of zeros
+  // Rows (metadata) are laid out per trial block in chunk order: the groups,
+  // in pairs (the u16 loop adds two per v_add3_u32), and a pad group wherever
+  // a group goes alone -- the last of an odd count, or one whose pair's
+  // windows do not fit a chunk buffer together.
+  std::vector<std::vector<int>> rows_of((size_t)n_dblk);  // per block: mt rows [row][ROW]
+  std::vector<std::vector<int>> chunks((size_t)n_dblk);
+  std::vector<std::vector<std::vector<std::array<int, 4>>>> cw((size_t)n_dblk);
+  auto gran = [&](int span) -> int64_t { return (Tq + span + 63) / 64 * 64; };
+  int64_t rows_pb = 0;
+  for (int64_t b = 0; b < n_dblk; ++b) {
+    std::vector<int>& M = rows_of[(size_t)b];
+    int64_t r0 = 0, nrow = 0, used = 0;
+    std::vector<std::array<int, 4>> rec;  // the open chunk's window records
+    auto close = [&]() {
+      if (nrow == 0) return;
+      for (int64_t r = r0; r < r0 + nrow; ++r) M[(size_t)(r * ROW + DB + 3)] = (int)(r | (nrow << 20));
+      chunks[(size_t)b].push_back((int)(r0 | (nrow << 20)));
+      for (auto& x : rec) x[3] |= (int)rec.size() << 20;
+      cw[(size_t)b].push_back(rec);
+      rec.clear();
+      r0 += nrow;
+      nrow = 0;
+      used = 0;
+    };
+    // windows of group g in this block: {pattern row, bmin, span}, first-use order
+    auto windows = [&](int64_t g, std::vector<std::array<int, 3>>& w) {
+      w.clear();
+      if (g < 0 || g >= NG) {
+        w.push_back({zero_row, 0, 0});
+        return;
+      }
+      for (int64_t j = 0; j < DB; ++j) {
+        const int64_t d = std::min(b * DB + j, D - 1);
+        const int id = pid[(size_t)(d * NG + g)];
+        const int base = tab[d * C + g * kFx];
+        size_t i = 0;
+        while (i < w.size() && w[i][0] != id) ++i;
+        if (i == w.size()) w.push_back({id, base, base});
+        else {
+          w[i][1] = std::min(w[i][1], base);
+          w[i][2] = std::max(w[i][2], base);
+        }
+      }
+      for (auto& x : w) x[2] -= x[1];  // span
+    };
+    auto need_of = [&](const std::vector<std::array<int, 3>>& w) {
+      int64_t n = 0;
+      for (auto& x : w) n += gran(x[2]);
+      return n;
+    };
+    // one row (group g, or a pad group for g < 0) with its windows
+    auto place = [&](int64_t g, const std::vector<std::array<int, 3>>& w) {
+      const size_t base_row = M.size();
+      M.resize(base_row + (size_t)ROW, 0);
+      std::vector<int64_t> off(w.size());
+      for (size_t i = 0; i < w.size(); ++i) {
+        off[i] = used;
+        rec.push_back({w[i][1], (int)(Tq + w[i][2]), (int)used, w[i][0]});
+        used += gran(w[i][2]);
+      }
+      for (int64_t j = 0; j < DB; ++j) {
+        int o = (int)(16 * off[0]);
+        if (g >= 0 && g < NG) {
+          const int64_t d = std::min(b * DB + j, D - 1);
+          const int id = pid[(size_t)(d * NG + g)];
+          const int base = tab[d * C + g * kFx];
+          size_t i = 0;
+          while (w[i][0] != id) ++i;
+          o = (int)(16 * (off[i] + base - w[i][1]));
+        }
+        M[base_row + (size_t)j] = o;
+      }
+      ++nrow;
+    };
+    // a pair of rows into the open chunk (closing it first if they do not fit)
+    auto place_pair = [&](int64_t ga, const std::vector<std::array<int, 3>>& wa, int64_t gb,
+                          const std::vector<std::array<int, 3>>& wb) -> bool {
+      const int64_t need = need_of(wa) + need_of(wb);
+      const int64_t nwin = (int64_t)(wa.size() + wb.size());
+      if (need > buf_e || nwin > kFxWin) return false;
+      if (nrow + 2 > v.CC || used + need > buf_e || (int64_t)rec.size() + nwin > kFxWin) close();
+      place(ga, wa);
+      place(gb, wb);
+      return true;
+    };
+    std::vector<std::array<int, 3>> wa, wb, wz;
+    windows(-1, wz);
+    for (int64_t g = 0; g < NG; g += 2) {
+      windows(g, wa);
+      windows(g + 1, wb);  // g + 1 == NG: the pad group
+      if (place_pair(g, wa, g + 1 < NG ? g + 1 : -1, wb)) continue;
+      // the pair does not fit one buffer: each group with a pad group
+      if (!place_pair(g, wa, -1, wz)) return false;
+      if (g + 1 < NG && !place_pair(g + 1, wb, -1, wz)) return false;
+    }
+    close();
+    rows_pb = std::max(rows_pb, r0);
+  }
+  T.rows_pb = rows_pb;
+  T.mt.assign((size_t)(n_dblk * rows_pb * ROW), 0);
+  for (int64_t b = 0; b < n_dblk; ++b)
+    std::copy(rows_of[(size_t)b].begin(), rows_of[(size_t)b].end(),
+              T.mt.begin() + (size_t)(b * rows_pb * ROW));
+  size_t maxch = 0;
+  for (const auto& l : chunks) maxch = std::max(maxch, l.size());
+  T.maxch = (int)maxch;
+  T.cht.assign((size_t)(n_dblk * (maxch + 1)), 0);
+  T.wt.assign((size_t)(n_dblk * maxch * kFxWin * 4), 0);
+  for (int64_t b = 0; b < n_dblk; ++b) {
+    const auto& l = chunks[(size_t)b];
+    T.cht[(size_t)(b * (maxch + 1))] = (int)l.size();
+    for (size_t k = 0; k < l.size(); ++k) {
+      T.cht[(size_t)(b * (maxch + 1) + 1 + k)] = l[k];
+      const auto& r = cw[(size_t)b][k];
+      for (size_t i = 0; i < r.size(); ++i)
+        for (int f = 0; f < 4; ++f) T.wt[(((size_t)b * maxch + k) * kFxWin + i) * 4 + f] = r[i][f];
+    }
+  }
+  return true;
+}
+
+static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int64_t C, int dtype,
+                       int flags, pdd_sweep_plan** plan_out);
+
 int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int dtype,
                           pdd_sweep_plan** plan_out) {
-  return pdd_sweep_plan_create_grouped(host_table, 1, D, C, dtype, plan_out);
+  return plan_create(host_table, 1, D, C, dtype, PDD_SWEEP_FACTOR, plan_out);
+}
+
+int pdd_sweep_plan_create_ex(const int32_t* host_table, int64_t D, int64_t C, int dtype, int flags,
+                             pdd_sweep_plan** plan_out) {
+  return plan_create(host_table, 1, D, C, dtype, flags, plan_out);
 }
 
 int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int64_t D, int64_t C,
                                   int dtype, pdd_sweep_plan** plan_out) {
+  return plan_create(host_table, n_grp, D, C, dtype, 0, plan_out);
+}
+
+}  // extern "C"
+
+static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int64_t C, int dtype,
+                       int flags, pdd_sweep_plan** plan_out) {
   PDD_REQUIRE(host_table && plan_out, "pdd_sweep_plan_create: null pointer");
   PDD_REQUIRE(n_grp >= 1 && n_grp * C < (1 << 20), "pdd_sweep_plan_create: bad group count");
   PDD_REQUIRE(D > 0 && C > 0 && D < (1 << 24) && C < (1 << 20),
@@ -1624,6 +1926,29 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
         for (size_t k = 0; k < chunks[i].size(); ++k) bmin[i * (maxch + 1) + 1 + k] = chunks[i][k];
       }
       p->maxch = (int)maxch;
+      // 8-bit single-group sweeps: the factorised tables when they pay
+      FxTables T;
+      if ((flags & PDD_SWEEP_FACTOR) && dtype == PDD_U8 && n_grp == 1 && v.S == 8 &&
+          il_kernel_for(v, true) &&
+          fx_build(host_table, D, C, v, buf_e, (flags & PDD_SWEEP_FACTOR_FORCE) != 0, T)) {
+        p->fx = kFx;
+        p->n_pat = T.n_pat;
+        p->fx_rows = T.rows_pb;
+        p->maxch = T.maxch;
+        tab.swap(T.mt);
+        bmin.swap(T.cht);
+        hipError_t e = hipMalloc(&p->d_pat, T.pat.size() * sizeof(int));
+        if (e == hipSuccess) e = hipMalloc(&p->d_wt, T.wt.size() * sizeof(int));
+        if (e == hipSuccess)
+          e = hipMemcpy(p->d_pat, T.pat.data(), T.pat.size() * sizeof(int), hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+          e = hipMemcpy(p->d_wt, T.wt.data(), T.wt.size() * sizeof(int), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+          set_error("pdd_sweep_plan_create: %s", hipGetErrorString(e));
+          pdd_sweep_plan_destroy(p);
+          return -2;
+        }
+      }
     }
     p->max_bin = mx;
     p->min_bin = mn;
@@ -1639,7 +1964,7 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
       return -2;
     }
     if (p->lds_bytes > 64 * 1024) {
-      const void* kf = il ? (const void*)il_kernel_for(v) : (const void*)kernel_for(v);
+      const void* kf = il ? (const void*)il_kernel_for(v, p->fx != 0) : (const void*)kernel_for(v);
       e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, p->lds_bytes);
       if (e != hipSuccess) {
         set_error("pdd_sweep_plan_create: hipFuncSetAttribute: %s", hipGetErrorString(e));
@@ -1652,6 +1977,14 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
   }
   set_error("pdd_sweep_plan_create: no variant");
   return -1;
+}
+
+extern "C" {
+
+int pdd_sweep_plan_factor(const pdd_sweep_plan* p, int64_t* n_patterns) {
+  PDD_REQUIRE(p, "pdd_sweep_plan_factor: null pointer");
+  if (n_patterns) *n_patterns = p->n_pat;
+  return p->fx;
 }
 
 int pdd_sweep_plan_info(const pdd_sweep_plan* p, int64_t* info) {
@@ -1863,6 +2196,8 @@ int pdd_sweep_plan_destroy(pdd_sweep_plan* p) {
   if (p->d_tab) (void)hipFree(p->d_tab);
   if (p->d_bmin) (void)hipFree(p->d_bmin);
   if (p->d_bspan) (void)hipFree(p->d_bspan);
+  if (p->d_pat) (void)hipFree(p->d_pat);
+  if (p->d_wt) (void)hipFree(p->d_wt);
   if (p->d_meta) (void)hipFree(p->d_meta);
   if (p->d_win) (void)hipFree(p->d_win);
   if (p->d_rows) (void)hipFree(p->d_rows);

@@ -58,11 +58,15 @@ class DMSweep(object):
     [C, N] device tensor of that dtype (int16 / uint16 storage for 'u16') or
     a ``Spectra``."""
 
-    def __init__(self, dms, freqs, dt, cur_dm=0.0, dtype="f32", input_max=None):
+    def __init__(self, dms, freqs, dt, cur_dm=0.0, dtype="f32", input_max=None, factor=True):
         """``input_max`` (integer dtypes): the largest sample value the input
         and its integer pads hold (default 255 for 'u8', 1023 for 'u16'); a
         tighter bound lets the exact packed-u16 accumulation convert less
-        often (pdd_sweep_plan_set_input_max)."""
+        often (pdd_sweep_plan_set_input_max).  ``factor``: 8-bit plans may
+        sweep exactly factorised over groups of 4 channels when that pays
+        (pdd_sweep_plan_create_ex PDD_SWEEP_FACTOR; bit-identical planes);
+        False forces the channel-by-channel kernel; "force" factorises even
+        where it does not pay (tests of small grids)."""
         _lib.require_gpu()
         self.dms = np.atleast_1d(np.asarray(dms, dtype=np.float64))
         self.freqs = np.asarray(freqs, dtype=np.float64)
@@ -75,6 +79,7 @@ class DMSweep(object):
         self.max_bin = int(self.table.max()) if self.table.size else 0
         self.dtype = dtype
         self.input_max = None if input_max is None else int(input_max)
+        self.factor = factor if factor == "force" else bool(factor)
         if self.input_max is not None:
             assert dtype in ("u8", "u16") and 1 <= self.input_max <= (255 if dtype == "u8" else 1023)
         self._plans = {}
@@ -84,9 +89,11 @@ class DMSweep(object):
         if p is None:
             h = ctypes.c_void_p()
             tab = np.ascontiguousarray(self.table)
-            _lib.check(_lib.lib().pdd_sweep_plan_create(
-                tab.ctypes.data_as(ctypes.c_void_p), self.D, self.C, code, ctypes.byref(h)),
-                "pdd_sweep_plan_create")
+            _lib.check(_lib.lib().pdd_sweep_plan_create_ex(
+                tab.ctypes.data_as(ctypes.c_void_p), self.D, self.C, code,
+                (_lib.SWEEP_FACTOR | _lib.SWEEP_FACTOR_FORCE) if self.factor == "force"
+                else (_lib.SWEEP_FACTOR if self.factor else 0), ctypes.byref(h)),
+                "pdd_sweep_plan_create_ex")
             p = h
             self._plans[code] = p
             if self.input_max is not None and code != _lib.F32:
@@ -101,6 +108,15 @@ class DMSweep(object):
         keys = ("D", "C", "dms_per_block", "samples_per_block", "lds_bytes", "max_bin", "min_bin",
                 "variant")
         return dict(zip(keys, (int(v) for v in a)))
+
+    def factor_info(self, code=_lib.U8):
+        """(channels per factor group, stage-1 patterns) of the plan for
+        ``code``; (0, 0) for a channel-by-channel plan."""
+        n = ctypes.c_int64(0)
+        g = _lib.lib().pdd_sweep_plan_factor(self._plan(code), ctypes.byref(n))
+        if g < 0:
+            _lib.check(g, "pdd_sweep_plan_factor")
+        return int(g), int(n.value)
 
     def n_out(self, N, trim=True):
         if trim and self.max_bin > 0:

@@ -1,0 +1,103 @@
+"""Exact factorised 8-bit sweep (pdd_sweep.hip k_fx_patterns + k_sweep_il
+FX): each group of 4 adjacent channels is summed once per distinct
+relative-shift pattern, and every trial adds its pattern series at the
+group's base shift -- the same integer samples as the channel-by-channel sum
+(formats/spectra.py:229-260 dedisperse + bin/waterfaller.py:140 channel sum,
+per trial), so the planes must be BIT-IDENTICAL to the oracle's and to the
+channel-by-channel kernel's."""
+import numpy as np
+import pytest
+
+from conftest import band, u8_data
+from oracle import spectra_oracle as orc
+
+DT = 64e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pad", [0, 7, "rotate"])
+@pytest.mark.parametrize("descending", [True, False])
+@pytest.mark.parametrize("C", [32, 36])
+def test_factor_small_grids_vs_oracle(gpu, pad, descending, C):
+    """Forced factorisation on small grids: pads (value / rotate) past the
+    block edge (trim=False), ascending bands (negative relative shifts), an
+    odd group count (C = 36: 9 groups, the last pair ends in a zero group)."""
+    import torch
+    from pypulsar_amd.sweep import DMSweep
+    N, D = 6000, 64
+    freqs = band(C, descending=descending)
+    x = u8_data(C, N, 31 + C)
+    # (a grid whose group pairs' pattern windows fit one chunk buffer: with
+    # 9-MHz channels every trial of a wider grid has its own pattern)
+    dms = np.linspace(0, 3.0 if C == 32 else 4.0, D)
+    sw = DMSweep(dms, freqs, DT, dtype="u8", factor="force")
+    assert sw.factor_info()[0] == 4
+    for trim in (True, False):
+        plane = sw(torch.from_numpy(x).cuda(), padval=pad, trim=trim).cpu().numpy()
+        tab = orc.sweep_table(dms, freqs, DT)
+        n_out = plane.shape[1]
+        want = orc.sweep_plane(x.astype(np.float64), tab, pad, n_out=n_out)
+        np.testing.assert_array_equal(plane.astype(np.float64), want,
+                                      err_msg="pad %r trim %s" % (pad, trim))
+    sw.close()
+
+
+@pytest.mark.gpu
+def test_factor_config1_geometry_equals_channel_sweep(gpu):
+    """BASELINE configs[1] geometry (1024 ch x 1024 DM, 0-1000 pc/cc) on 8-bit
+    data at N = 2^17: the planner factorises on its own (4 channels per group),
+    and the plane equals the channel-by-channel kernel's bit for bit, and the
+    oracle's rows."""
+    import torch
+    from pypulsar_amd.sweep import DMSweep
+    C, N, D = 1024, 1 << 17, 1024
+    freqs = band(C)
+    dms = np.linspace(0, 1000, D)
+    x = u8_data(C, N, 41)
+    xd = torch.from_numpy(x).cuda()
+    fx = DMSweep(dms, freqs, DT, dtype="u8")
+    g, n_pat = fx.factor_info()
+    assert g == 4 and 0 < n_pat < 16 * C
+    plain = DMSweep(dms, freqs, DT, dtype="u8", factor=False)
+    assert plain.factor_info()[0] == 0
+    a = fx(xd)
+    b = plain(xd)
+    assert torch.equal(a, b)
+    tab = orc.sweep_table(dms, freqs, DT)
+    rows = [0, 1, 511, 777, 1023]
+    want = orc.sweep_plane(x.astype(np.float64), tab[rows], 0, n_out=a.shape[1])
+    np.testing.assert_array_equal(a[rows].cpu().numpy().astype(np.float64), want)
+    fx.close()
+    plain.close()
+
+
+@pytest.mark.gpu
+def test_factor_segments_and_column_offsets(gpu, monkeypatch):
+    """A segment budget that splits the factorised sweep into several
+    launches (each with its own interleave + pattern image), and a column
+    range [x_off, x_off + n_out) swept from the pieces layout (the DM-sharded
+    path): both equal the one-shot channel-by-channel plane."""
+    import torch
+    from pypulsar_amd.sweep import DMSweep
+    C, N, D = 1024, 1 << 16, 512
+    freqs = band(C)
+    dms = np.linspace(0, 500, D)
+    x = u8_data(C, N, 43)
+    xd = torch.from_numpy(x).cuda()
+    plain = DMSweep(dms, freqs, DT, dtype="u8", factor=False)
+    ref = plain(xd)
+    fx = DMSweep(dms, freqs, DT, dtype="u8")
+    assert fx.factor_info()[0] == 4
+    monkeypatch.setenv("PDD_SWEEP_SEG_BYTES", str(3 << 28))
+    seg = fx(xd)
+    monkeypatch.delenv("PDD_SWEEP_SEG_BYTES")
+    assert torch.equal(seg, ref)
+    # pieces layout [N/P][C][P] and a column window
+    P = 1 << 13
+    xp = xd.view(C, N // P, P).permute(1, 0, 2).contiguous()
+    x_off, n_cols = 3000, 20000
+    out = torch.empty((D, n_cols), dtype=torch.float32, device="cuda")
+    fx.sweep_pieces(xp, N, P, x_off, n_cols, out)
+    assert torch.equal(out, ref[:, x_off:x_off + n_cols])
+    fx.close()
+    plain.close()
