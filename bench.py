@@ -269,6 +269,8 @@ def main():
                     help="stream: zero-DM mode (auto = 'wrap', the reference's uint8 result of "
                          "zero_dm_filter.py:30-39, on the exact 16-bit path)")
     ap.add_argument("--cpu-trials", type=int, default=None)
+    ap.add_argument("--no-factor", action="store_true",
+                    help="8-bit sweeps channel by channel (no exact 4-channel factorisation)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true",
                     help="dmshard: skip the PCIe-inclusive (pinned host -> H2D -> step) leg")
@@ -337,7 +339,8 @@ def sweep_bench(args, cfg, rank, world, dev):
         # uniform grid = one DDstep at downsamp 1: every trial weighs 1/1
         # (DDplan2b.py:272-273); DMShardedSweep balances the slices by it
         ds = DMShardedSweep(dms_all, freqs, dt, N, dtype=tdt, n_batches=nb,
-                            work=trial_work(dms_all, 1), gather=args.gather, device=dev)
+                            work=trial_work(dms_all, 1), gather=args.gather, device=dev,
+                            factor=not args.no_factor)
         log("rank %d: DM slice [%d, %d) of %d, %d batch(es)" % (rank, ds.lo, ds.hi, D, nb))
         # this rank's H2D share of every time batch, [nb, N/(nb*world), C],
         # in file (time-major) order
@@ -349,7 +352,7 @@ def sweep_bench(args, cfg, rank, world, dev):
             return ds(part)
     else:
         x = synth_block(C, N, 1000 + rank, dtype, dev)
-        sw = DMSweep(dms_all, freqs, dt, dtype=dtype)
+        sw = DMSweep(dms_all, freqs, dt, dtype=dtype, factor=not args.no_factor)
         rows, n_out = D, sw.n_out(N)
         plane = torch.empty((D, n_out), dtype=torch.float32, device=dev)
 
@@ -457,7 +460,13 @@ def sweep_bench(args, cfg, rank, world, dev):
     units_all = D * n_out * C * (world if mode == "timeblock" else 1)
     value = units_all * steps / el
     s_in = 1 if dtype == "u8" else 4
-    achieved = adds_rank_step * steps / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else None
+    # exact factorised 8-bit sweep: the kernel adds one
+    # pattern sample per (trial, group of fx channels), so its own adds are
+    # C / fx per samp*DM; the algorithmic rate is reported beside them
+    fx_g, fx_pat = sw.factor_info() if (sw is not None and dtype == "u8") else (0, 0)
+    kern_adds_step = rows * n_out * (C // fx_g) if fx_g else adds_rank_step
+    achieved = kern_adds_step * steps / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else None
+    effective = adds_rank_step * steps / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else None
     # LDS roof (the binding one): ds_read_b128 at 256 B/clk/CU
     # feeds 4 f32 samples (f32 quarters) or 8 u16 samples (u16 eighths) per 16 B
     lds_roof = N_CU * CLK_GHZ * 1e9 * LDS_B_PER_CLK / 16 * (8 if dtype == "u8" else 4) / 1e12
@@ -500,23 +509,36 @@ def sweep_bench(args, cfg, rank, world, dev):
                        "config_name": args.config, "channels": C, "samples": N, "dm_trials": D,
                        "n_out": n_out, "parallelism": "%s%d" % ("tb" if mode == "timeblock"
                                                                 else "dm", world),
-                       "rccl_world_size": rccl_world, "plan": plan},
+                       "rccl_world_size": rccl_world, "plan": plan,
+                       "method": ("exact factorisation over groups of %d channels (%d pattern "
+                                  "series; plane bit-identical to the channel-by-channel sum)"
+                                  % (fx_g, fx_pat) if fx_g else "channel by channel")},
             "roofline": {"bound": "lds", "achieved": achieved, "peak": lds_roof,
                          "unit": "T adds/s", "frac": achieved / lds_roof if achieved else None,
                          "traffic": traffic,
                          "traffic_source": ("profiles/pmc_sweep.json[%s] (separate rocprofv3 "
                                             "--pmc FETCH_SIZE / WRITE_SIZE passes of this "
                                             "command)" % pmc_key) if traffic else None,
-                         "kernel": "pdd::k_sweep_il", "kernel_ms_per_launch":
+                         "kernel": ("pdd::k_sweep_il (factorised stage 2)" if fx_g
+                                    else "pdd::k_sweep_il"), "kernel_ms_per_launch":
                              kern_ms / launches if launches else None,
                          "launches_per_step": launches / steps if launches else None,
                          "kernel_s_per_step": k_s,
-                         "adds_per_step_rank0": adds_rank_step,
-                         "note": "one add per samp*ch*DM, no MFMA-shaped work; every add reads "
-                                 "its sample from the LDS image (ds_read_b128: %d samples per 16 B "
-                                 "at 256 B/clk/CU = the peak, in adds/s), which binds; the VALU "
-                                 "issue rate (SIMD-32, MI355X_MICROARCH.md:53-54) is beside it "
-                                 "(DESIGN.md §3-4)" % (8 if dtype == "u8" else 4),
+                         "adds_per_step_rank0": kern_adds_step,
+                         "units_per_step_rank0": adds_rank_step,
+                         "effective_units_T_per_s": effective,
+                         "note": ("factorised stage 2: one add per samp*DM*(group of %d "
+                                  "channels), each reading its pattern sample from the LDS image "
+                                  "(ds_read_b128: 8 samples per 16 B at 256 B/clk/CU = the peak, "
+                                  "in adds/s); the tile is bound by staging the pattern windows "
+                                  "(LDS-DMA), so the LDS-read fraction is low by construction; "
+                                  "effective_units_T_per_s = samp*ch*DM per second of this "
+                                  "kernel (DESIGN.md §3)" % fx_g) if fx_g else
+                                 ("one add per samp*ch*DM, no MFMA-shaped work; every add reads "
+                                  "its sample from the LDS image (ds_read_b128: %d samples per 16 B "
+                                  "at 256 B/clk/CU = the peak, in adds/s), which binds; the VALU "
+                                  "issue rate (SIMD-32, MI355X_MICROARCH.md:53-54) is beside it "
+                                  "(DESIGN.md §3-4)" % (8 if dtype == "u8" else 4)),
                          "lds_bytes_per_add": 2 if dtype == "u8" else 4,
                          "valu": {"peak": valu_roof, "unit": "T adds/s",
                                   "instr": ("v_add3_u32 over a channel pair of packed u16 samples "
@@ -591,7 +613,7 @@ def rehearse_bench(args, cfg, dev):
 
     # the N = 1 step (whole grid, one rank, nb = 1 as in the default bench line)
     ds1 = DMShardedSweep(dms, freqs, dt, N, dtype=tdt, n_batches=1, work=trial_work(dms, 1),
-                         device=dev)
+                         device=dev, factor=not args.no_factor)
     t1, k1, l1 = timed(ds1, block.view(1, N, C))
     db = ds1.sw.info(1 if dtype == "u8" else 0)["dms_per_block"]
     ds1.close()
@@ -601,7 +623,7 @@ def rehearse_bench(args, cfg, dev):
     ranks, shared = [], None
     for r in range(W):
         ds = DMShardedSweep(dms, freqs, dt, N, dtype=tdt, n_batches=nb, work=trial_work(dms, 1),
-                            device=dev, world=W, rank=r, x_buf=shared)
+                            device=dev, world=W, rank=r, x_buf=shared, factor=not args.no_factor)
         if shared is None:
             ds.prefill(block)
             shared = ds.x

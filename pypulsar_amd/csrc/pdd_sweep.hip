@@ -685,6 +685,46 @@ __global__ __launch_bounds__(256) void k_fx_patterns(const uint4* __restrict__ R
   }
 }
 
+// Stage 1 through LDS: one workgroup per (group, kFxE-element block) loads
+// the group's four rows over the block (+ the group's relative-shift range)
+// ONCE and writes every pattern of the group from them (the plain kernel
+// above reads four rows per pattern element from L2: 4 x 16 B per 16 B
+// written).  gtab: [NG + 1] first pattern of each group, then [NG] x {lo,
+// hi} = the group's min(0, r) / max(0, r) over its patterns (hi - lo <=
+// kFxRspan, checked by the plan).
+constexpr int kFxE = 512, kFxRspan = 512;
+__global__ __launch_bounds__(256) void k_fx_patterns_lds(const uint4* __restrict__ R, int64_t nR,
+                                                         const int4* __restrict__ pat,
+                                                         const int* __restrict__ gtab, int NG,
+                                                         uint4* __restrict__ P) {
+  extern __shared__ __attribute__((aligned(16))) uint4 L[];
+  const int g = blockIdx.x;
+  const int64_t j0 = (int64_t)blockIdx.y * kFxE;
+  const int p0 = gtab[g], p1 = gtab[g + 1];
+  const int lo = gtab[NG + 1 + 2 * g], hi = gtab[NG + 2 + 2 * g];
+  const int W = kFxE + hi - lo;
+  const uint4* r0 = R + (int64_t)(g * kFx) * nR;
+#pragma unroll
+  for (int k = 0; k < kFx; ++k)
+    for (int e = threadIdx.x; e < W; e += 256) {
+      const int64_t i = j0 + lo + e;
+      L[k * W + e] = (i >= 0 && i < nR) ? r0[(int64_t)k * nR + i] : make_uint4(0u, 0u, 0u, 0u);
+    }
+  __syncthreads();
+  for (int p = p0; p < p1; ++p) {
+    const int4 q = pat[p];
+#pragma unroll
+    for (int e = threadIdx.x; e < kFxE; e += 256) {
+      const int64_t j = j0 + e;
+      if (j >= nR) break;
+      const uint4 a = L[e - lo], b = L[W + e - lo + q.y], c = L[2 * W + e - lo + q.z],
+                  d = L[3 * W + e - lo + q.w];
+      P[(int64_t)p * nR + j] = make_uint4(a.x + b.x + c.x + d.x, a.y + b.y + c.y + d.y,
+                                          a.z + b.z + c.z + d.z, a.w + b.w + c.w + d.w);
+    }
+  }
+}
+
 // n DMAs of 64 elements (1 KiB) each, q = first, first + step, ...
 __device__ __forceinline__ int stage_il_dma(uint32_t lds_dst, const float4* src, int ne, int first,
                                             int step, int lane) {
@@ -864,13 +904,41 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   (void)R; (void)t0; (void)mt_b;
   const int tile = blockIdx.x;
   IL_TILE_SETUP
+  // FX tiles: the chunk's window records (lane i = window i, one vector
+  // load), and one wave's share of a chunk's window DMAs.  (Measured and
+  // dropped: every wave of the workgroup issuing a share of the DMAs -- the
+  // compute waves' stage-2 work is a quarter of the channel sweep's --
+  // configs[3] 101.6 -> 116.4 ms per launch: the staging does not scale
+  // with the issuing waves.)
+  const uint32_t img_lds = lds_addr_of(img);
+  const int4* wt_b = FX ? wt + ((int64_t)grp * n_dblk + dblk) * maxch * kFxWin : nullptr;
+  auto fx_rec = [&](int k) -> int4 {
+    if constexpr (FX) return wt_b[(int64_t)min(k, nchunk - 1) * kFxWin + lane];
+    else return make_int4(0, 0, 0, 0);
+  };
+  auto fx_issue = [&](int k, const int4& rec, int first, int step) -> int {
+    // the compiler's wait for the record (vmcnt(0): it cannot see the DMAs)
+    // lands here, before any DMA of this chunk
+    asm volatile("" ::"v"(rec.x), "v"(rec.y), "v"(rec.z), "v"(rec.w));
+    const int b = k % NBUF;
+    const int nw = __builtin_amdgcn_readlane(rec.w, 0) >> 20;
+    int n = 0;
+    for (int i = 0; i < nw; ++i) {
+      const int bm = __builtin_amdgcn_readlane(rec.x, i);
+      const int len = __builtin_amdgcn_readlane(rec.y, i);
+      const int off = __builtin_amdgcn_readlane(rec.z, i);
+      const int row = __builtin_amdgcn_readlane(rec.w, i) & 0xfffff;
+      n += stage_il_dma(img_lds + (uint32_t)((b * buf_e + off) * 16),
+                        R + (int64_t)row * nR + (t0 + bm - lo), len, first, step, lane);
+    }
+    return n;
+  };
   if (w >= NCW) {
     // ---------------- loader waves: metadata rows + sample windows
     // Top issue priority: a loader shares its SIMD with compute waves that
     // have an LDS read or add ready every cycle.
     if (!(dbg & 8)) __builtin_amdgcn_s_setprio(3);
     const int lw = w - NCW;
-    const uint32_t img_lds = lds_addr_of(img);
     int* ring = metar;  // the shared ring (loader 0 fills it)
     // chunk k = channels c0 .. c0 + ncc - 1 (cht: c0 | ncc << 20), packed
     // into its buffer at the per-channel offsets of the metadata rows
@@ -892,33 +960,16 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       }
       return n;
     };
-    // FX: the chunk's window records, lane i = window i (vector load)
-    const int4* wt_b = FX ? wt + ((int64_t)grp * n_dblk + dblk) * maxch * kFxWin : nullptr;
-    auto load_rec = [&](int k) -> int4 {
-      if constexpr (FX) return wt_b[(int64_t)min(k, nchunk - 1) * kFxWin + lane];
-      else return make_int4(0, 0, 0, 0);
-    };
-    int4 rec_next = load_rec(0);
+    int4 rec_next = fx_rec(0);
     auto issue_samples = [&](int k) -> int {
       if (dbg & 1) return 0;
       if constexpr (FX) {
         // the record of chunk k was loaded an iteration ahead (the wait for
         // it is the one this iteration already did); load chunk k + 1's now
         const int4 rec = rec_next;
-        asm volatile("" ::"v"(rec.x), "v"(rec.y), "v"(rec.z), "v"(rec.w));
-        const int b = k % NBUF;
-        const int nw = __builtin_amdgcn_readlane(rec.w, 0) >> 20;
-        int n = 0;
-        for (int i = 0; i < nw; ++i) {
-          const int bm = __builtin_amdgcn_readlane(rec.x, i);
-          const int len = __builtin_amdgcn_readlane(rec.y, i);
-          const int off = __builtin_amdgcn_readlane(rec.z, i);
-          const int row = __builtin_amdgcn_readlane(rec.w, i) & 0xfffff;
-          n += stage_il_dma(img_lds + (uint32_t)((b * buf_e + off) * 16),
-                            R + (int64_t)row * nR + (t0 + bm - lo), len, lw, NLW, lane);
-        }
+        int n = fx_issue(k, rec, lw, NLW);
         if (k + 1 < nchunk) {
-          rec_next = load_rec(k + 1);
+          rec_next = fx_rec(k + 1);
           ++n;  // rides on the counted vmcnt
         }
         return n;
@@ -1046,6 +1097,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       tA = __builtin_amdgcn_s_memtime();
       ts_comp += tA - tB;
     }
+
 #ifdef PDD_SWEEP_DEV
     if (!(dbg & 64))
 #endif
@@ -1376,6 +1428,7 @@ struct pdd_sweep_plan {
   int64_t fx_rows = 0;     // factorised: metadata rows per trial block (groups + pad groups)
   int* d_pat = nullptr;    // factorised: [n_pat][4] {c0, r1, r2, r3}
   int* d_wt = nullptr;     // factorised: [n_dblk][maxch][kFxWin][4] window records
+  int* d_gtab = nullptr;   // factorised: per group first pattern + relative-shift range (LDS stage 1)
   int dtype = PDD_F32;     // input element type
   int input_max = 0;       // largest input value (integer input; 0 = the dtype's bound)
   int64_t n_grp = 1;       // independent channel groups (grouped sweep)
@@ -1530,8 +1583,15 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
         rc = -3;
         break;
       }
-      hipLaunchKernelGGL(k_fx_patterns, dim3((unsigned)p->n_pat, (unsigned)cdiv(nR, 256 * kIlPer)),
-                         dim3(256), 0, st, (const uint4*)R, nR, (const int4*)p->d_pat, P);
+      if (p->d_gtab) {
+        const int NG = (int)(p->C / p->fx);
+        hipLaunchKernelGGL(k_fx_patterns_lds, dim3((unsigned)NG, (unsigned)cdiv(nR, kFxE)), dim3(256),
+                           (size_t)(kFx * (kFxE + kFxRspan)) * sizeof(uint4), st, (const uint4*)R, nR,
+                           (const int4*)p->d_pat, p->d_gtab, NG, P);
+      } else {
+        hipLaunchKernelGGL(k_fx_patterns, dim3((unsigned)p->n_pat, (unsigned)cdiv(nR, 256 * kIlPer)),
+                           dim3(256), 0, st, (const uint4*)R, nR, (const int4*)p->d_pat, P);
+      }
       if (hipGetLastError() != hipSuccess) { rc = -3; break; }
     }
     const int64_t n_tblk = Qs / Tq;
@@ -1568,9 +1628,10 @@ extern "C" {
 // tables, and the window records of every chunk.  Returns false when a chunk
 // cannot hold a group pair's windows or the factorisation does not pay.
 struct FxTables {
-  std::vector<int> pat, mt, cht, wt;
+  std::vector<int> pat, mt, cht, wt, gtab;  // gtab empty: a group's shift range exceeds kFxRspan
   int64_t n_pat = 0, rows_pb = 0;  // metadata rows per trial block
   int maxch = 0;
+  double cost_b = 0, cost_f = 0;   // modelled cycles per time tile: channel sweep / factorised
 };
 static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v, int64_t buf_e,
                      bool force, FxTables& T) {
@@ -1605,8 +1666,26 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
     }
   }
   T.n_pat = (int64_t)T.pat.size() / 4;
-  // pays when stage 1 (4 adds per pattern sample) + stage 2 (one add per
-  // trial and group) is at most half of the channel sweep's adds
+  {
+    // per group: first pattern, then the relative-shift range (stage 1 via LDS)
+    T.gtab.assign((size_t)(NG + 1 + 2 * NG), 0);
+    bool fits = true;
+    int64_t g = -1;
+    for (int64_t p = 0; p < T.n_pat; ++p) {
+      const int64_t pg = T.pat[(size_t)(4 * p)] / kFx;
+      while (g < pg) T.gtab[(size_t)(++g)] = (int)p;
+      int& lo = T.gtab[(size_t)(NG + 1 + 2 * pg)];
+      int& hi = T.gtab[(size_t)(NG + 2 + 2 * pg)];
+      for (int k = 1; k < kFx; ++k) {
+        lo = std::min(lo, T.pat[(size_t)(4 * p + k)]);
+        hi = std::max(hi, T.pat[(size_t)(4 * p + k)]);
+      }
+      if (hi - lo > kFxRspan) fits = false;
+    }
+    while (g < NG) T.gtab[(size_t)(++g)] = (int)T.n_pat;
+    if (!fits) T.gtab.clear();
+  }
+  // (a quick screen: stage 1 + stage 2 adds against the channel sweep's)
   if (!force && (double)T.n_pat * kFx + (double)D * NG > 0.5 * (double)D * C) return false;
   if (T.n_pat + 1 >= (1 << 20)) return false;
   const int zero_row = (int)T.n_pat;  // pad groups read a window of this row of zeros
@@ -1619,6 +1698,7 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
   std::vector<std::vector<std::vector<std::array<int, 4>>>> cw((size_t)n_dblk);
   auto gran = [&](int span) -> int64_t { return (Tq + span + 63) / 64 * 64; };
   int64_t rows_pb = 0;
+  double cost_b = 0, cost_f = 0;
   for (int64_t b = 0; b < n_dblk; ++b) {
     std::vector<int>& M = rows_of[(size_t)b];
     int64_t r0 = 0, nrow = 0, used = 0;
@@ -1707,7 +1787,34 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
     }
     close();
     rows_pb = std::max(rows_pb, r0);
+    // cost model of one tile of this trial block (CU cycles; calibrated on
+    // MI355X for the u16 tiling, BASELINE configs[3] round 3): the channel
+    // sweep's compute waves take ~440 cycles per channel and its loaders
+    // ~1.15 per staged element (LDS-DMA issue), with ~15% synchronisation
+    // (2.06 M cycles per configs[3] tile); the factorised stage 2 has a
+    // quarter of the compute and is loader-bound at ~1.44 x its staging
+    // (1.37 M cycles per configs[3] tile)
+    int64_t el_b = 0, el_f = 0;  // staged elements: channel sweep / factorised
+    for (int64_t c = 0; c < C; ++c) {
+      int lo_ = INT32_MAX, hi_ = INT32_MIN;
+      for (int64_t j = 0; j < DB; ++j) {
+        const int x = tab[std::min(b * DB + j, D - 1) * C + c];
+        lo_ = std::min(lo_, x);
+        hi_ = std::max(hi_, x);
+      }
+      el_b += gran(hi_ - lo_);
+    }
+    for (const auto& ch : cw[(size_t)b])
+      for (const auto& r : ch) el_f += (r[1] + 63) / 64 * 64;
+    cost_b += 1.15 * std::max(440.0 * (double)C, 1.15 * (double)el_b);
+    cost_f += 1.44 * std::max(110.0 * (double)C, 1.15 * (double)el_f);
   }
+  // stage 1 per time tile: every pattern's 2 KiB of eighths, written once
+  // for all trial blocks at ~6.7 B per CU cycle (k_fx_patterns_lds: 4.1 TB/s)
+  cost_f += (double)T.n_pat * 2048.0 / 6.7;
+  T.cost_b = cost_b;
+  T.cost_f = cost_f;
+  if (!force && cost_f > 0.9 * cost_b) return false;
   T.rows_pb = rows_pb;
   T.mt.assign((size_t)(n_dblk * rows_pb * ROW), 0);
   for (int64_t b = 0; b < n_dblk; ++b)
@@ -1943,6 +2050,13 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
           e = hipMemcpy(p->d_pat, T.pat.data(), T.pat.size() * sizeof(int), hipMemcpyHostToDevice);
         if (e == hipSuccess)
           e = hipMemcpy(p->d_wt, T.wt.data(), T.wt.size() * sizeof(int), hipMemcpyHostToDevice);
+        if (e == hipSuccess && !T.gtab.empty()) e = hipMalloc(&p->d_gtab, T.gtab.size() * sizeof(int));
+        if (e == hipSuccess && !T.gtab.empty())
+          e = hipMemcpy(p->d_gtab, T.gtab.data(), T.gtab.size() * sizeof(int), hipMemcpyHostToDevice);
+        if (e == hipSuccess && !T.gtab.empty())
+          e = hipFuncSetAttribute((const void*)k_fx_patterns_lds,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)(kFx * (kFxE + kFxRspan) * sizeof(uint4)));
         if (e != hipSuccess) {
           set_error("pdd_sweep_plan_create: %s", hipGetErrorString(e));
           pdd_sweep_plan_destroy(p);
@@ -2198,6 +2312,7 @@ int pdd_sweep_plan_destroy(pdd_sweep_plan* p) {
   if (p->d_bspan) (void)hipFree(p->d_bspan);
   if (p->d_pat) (void)hipFree(p->d_pat);
   if (p->d_wt) (void)hipFree(p->d_wt);
+  if (p->d_gtab) (void)hipFree(p->d_gtab);
   if (p->d_meta) (void)hipFree(p->d_meta);
   if (p->d_win) (void)hipFree(p->d_win);
   if (p->d_rows) (void)hipFree(p->d_rows);

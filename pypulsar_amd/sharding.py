@@ -170,7 +170,7 @@ class DMShardedSweep(object):
 
     def __init__(self, dms, freqs, dt, N, dtype=torch.uint8, n_batches=1, work=None,
                  gather=False, dst=0, group=None, device=None, to_cm=None, sweep_fn=None,
-                 pieces=None, world=None, rank=None, x_buf=None, gather_fn=None):
+                 pieces=None, world=None, rank=None, x_buf=None, gather_fn=None, factor=True):
         from . import delays as _delays
         self.group = group
         self.rehearse = world is not None
@@ -249,7 +249,8 @@ class DMShardedSweep(object):
             from .sweep import DMSweep
             code = "u8" if dtype == torch.uint8 else "f32"
             if self.rows:
-                self.sw = DMSweep(self.dms[self.lo:self.hi], self.freqs, dt, dtype=code)
+                self.sw = DMSweep(self.dms[self.lo:self.hi], self.freqs, dt, dtype=code,
+                                  factor=factor)
 
             def sweep_fn(x, N, piece, x_off, dms_slice, out, n_cols):
                 if piece:

@@ -45,8 +45,9 @@ def test_factor_small_grids_vs_oracle(gpu, pad, descending, C):
 @pytest.mark.gpu
 def test_factor_config1_geometry_equals_channel_sweep(gpu):
     """BASELINE configs[1] geometry (1024 ch x 1024 DM, 0-1000 pc/cc) on 8-bit
-    data at N = 2^17: the planner factorises on its own (4 channels per group),
-    and the plane equals the channel-by-channel kernel's bit for bit, and the
+    data at N = 2^17, factorised (forced: at dDM ~ 1 the planner's cost model
+    keeps this grid on the channel kernel, 25k patterns for 256 groups): the
+    plane equals the channel-by-channel kernel's bit for bit, and the
     oracle's rows."""
     import torch
     from pypulsar_amd.sweep import DMSweep
@@ -55,9 +56,10 @@ def test_factor_config1_geometry_equals_channel_sweep(gpu):
     dms = np.linspace(0, 1000, D)
     x = u8_data(C, N, 41)
     xd = torch.from_numpy(x).cuda()
-    fx = DMSweep(dms, freqs, DT, dtype="u8")
+    assert DMSweep(dms, freqs, DT, dtype="u8").factor_info()[0] == 0
+    fx = DMSweep(dms, freqs, DT, dtype="u8", factor="force")
     g, n_pat = fx.factor_info()
-    assert g == 4 and 0 < n_pat < 16 * C
+    assert g == 4 and 0 < n_pat < 32 * C
     plain = DMSweep(dms, freqs, DT, dtype="u8", factor=False)
     assert plain.factor_info()[0] == 0
     a = fx(xd)
@@ -86,9 +88,13 @@ def test_factor_segments_and_column_offsets(gpu, monkeypatch):
     xd = torch.from_numpy(x).cuda()
     plain = DMSweep(dms, freqs, DT, dtype="u8", factor=False)
     ref = plain(xd)
-    fx = DMSweep(dms, freqs, DT, dtype="u8")
-    assert fx.factor_info()[0] == 4
-    monkeypatch.setenv("PDD_SWEEP_SEG_BYTES", str(3 << 28))
+    fx = DMSweep(dms, freqs, DT, dtype="u8", factor="force")
+    g, n_pat = fx.factor_info()
+    assert g == 4
+    # image rows (channels + patterns + zero rows) x (delay span + ~3000
+    # elements of eighths): three or four segments of N
+    rows = C + 1 + n_pat + 1
+    monkeypatch.setenv("PDD_SWEEP_SEG_BYTES", str(rows * 16 * (fx.max_bin + 64 + 3000)))
     seg = fx(xd)
     monkeypatch.delenv("PDD_SWEEP_SEG_BYTES")
     assert torch.equal(seg, ref)
@@ -101,3 +107,14 @@ def test_factor_segments_and_column_offsets(gpu, monkeypatch):
     assert torch.equal(out, ref[:, x_off:x_off + n_cols])
     fx.close()
     plain.close()
+
+
+@pytest.mark.gpu
+def test_factor_chosen_for_config3_grid(gpu):
+    """BASELINE configs[3] grid (4096 ch x 4096 DMs, 0-1000 pc/cc): the
+    planner's cost model takes the factorised sweep."""
+    from pypulsar_amd.sweep import DMSweep
+    sw = DMSweep(np.linspace(0, 1000, 4096), band(4096), DT, dtype="u8")
+    g, n_pat = sw.factor_info()
+    assert g == 4 and n_pat > 1024
+    sw.close()
