@@ -79,6 +79,12 @@ CONFIGS = {
 }
 
 
+def _factor_arg(args):
+    """DMSweep(factor=...) of the --factor option."""
+    return {"auto": True, "off": False, "2": 2, "4": 4, "force2": "force2",
+            "force4": "force4"}[args.factor]
+
+
 def log(*a):
     print("[bench %s]" % time.strftime("%H:%M:%S"), *a, file=sys.stderr, flush=True)
 
@@ -269,8 +275,11 @@ def main():
                     help="stream: zero-DM mode (auto = 'wrap', the reference's uint8 result of "
                          "zero_dm_filter.py:30-39, on the exact 16-bit path)")
     ap.add_argument("--cpu-trials", type=int, default=None)
-    ap.add_argument("--no-factor", action="store_true",
-                    help="8-bit sweeps channel by channel (no exact 4-channel factorisation)")
+    ap.add_argument("--factor", default="auto", choices=["auto", "off", "2", "4", "force2", "force4"],
+                    help="8-bit sweeps: exact factorisation over channel groups (auto = the "
+                         "planner's cost model picks 4, 2 or none; off = channel by channel; "
+                         "2 / 4 = that group size where it pays; force2 / force4 = that size "
+                         "wherever it fits)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true",
                     help="dmshard: skip the PCIe-inclusive (pinned host -> H2D -> step) leg")
@@ -340,7 +349,7 @@ def sweep_bench(args, cfg, rank, world, dev):
         # (DDplan2b.py:272-273); DMShardedSweep balances the slices by it
         ds = DMShardedSweep(dms_all, freqs, dt, N, dtype=tdt, n_batches=nb,
                             work=trial_work(dms_all, 1), gather=args.gather, device=dev,
-                            factor=not args.no_factor)
+                            factor=_factor_arg(args))
         log("rank %d: DM slice [%d, %d) of %d, %d batch(es)" % (rank, ds.lo, ds.hi, D, nb))
         # this rank's H2D share of every time batch, [nb, N/(nb*world), C],
         # in file (time-major) order
@@ -352,7 +361,7 @@ def sweep_bench(args, cfg, rank, world, dev):
             return ds(part)
     else:
         x = synth_block(C, N, 1000 + rank, dtype, dev)
-        sw = DMSweep(dms_all, freqs, dt, dtype=dtype, factor=not args.no_factor)
+        sw = DMSweep(dms_all, freqs, dt, dtype=dtype, factor=_factor_arg(args))
         rows, n_out = D, sw.n_out(N)
         plane = torch.empty((D, n_out), dtype=torch.float32, device=dev)
 
@@ -496,8 +505,9 @@ def sweep_bench(args, cfg, rank, world, dev):
             "dtype": dtype,
             "data": "synthetic (uint8 clip(round(N(128,16))) filterbank%s, generated on device)"
                     % ("" if dtype == "u8" else " as float32"),
-            "config": {"workload": "%s: brute-force DM sweep %d ch x 2^%d samples x %d DM "
-                                   "(%g-%g pc/cc), 64 us, 1250-1550 MHz, trim=True%s"
+            "config": {"workload": "%s: DM sweep %d ch x 2^%d samples x %d DM "
+                                   "(%g-%g pc/cc), 64 us, 1250-1550 MHz, trim=True, every plane "
+                                   "row = the brute-force per-trial channel sum%s"
                                    % ("BASELINE configs[%d]" % cfg["baseline_index"]
                                       if cfg["baseline_index"] is not None else args.config,
                                       C, int(np.log2(N)), D, cfg["dm_lo"], cfg["dm_hi"],
@@ -613,7 +623,7 @@ def rehearse_bench(args, cfg, dev):
 
     # the N = 1 step (whole grid, one rank, nb = 1 as in the default bench line)
     ds1 = DMShardedSweep(dms, freqs, dt, N, dtype=tdt, n_batches=1, work=trial_work(dms, 1),
-                         device=dev, factor=not args.no_factor)
+                         device=dev, factor=_factor_arg(args))
     t1, k1, l1 = timed(ds1, block.view(1, N, C))
     db = ds1.sw.info(1 if dtype == "u8" else 0)["dms_per_block"]
     ds1.close()
@@ -623,7 +633,7 @@ def rehearse_bench(args, cfg, dev):
     ranks, shared = [], None
     for r in range(W):
         ds = DMShardedSweep(dms, freqs, dt, N, dtype=tdt, n_batches=nb, work=trial_work(dms, 1),
-                            device=dev, world=W, rank=r, x_buf=shared, factor=not args.no_factor)
+                            device=dev, world=W, rank=r, x_buf=shared, factor=_factor_arg(args))
         if shared is None:
             ds.prefill(block)
             shared = ds.x

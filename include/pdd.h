@@ -187,9 +187,14 @@ int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int d
 /* with PDD_SWEEP_FACTOR: factorise whenever the windows fit, paying or not
  * (tests of small grids) */
 #define PDD_SWEEP_FACTOR_FORCE 2
+/* with PDD_SWEEP_FACTOR: groups of 2 channels only (default: 4 or 2, the
+ * cheaper by the plan's cost model; 2 where a 4-channel group's pattern
+ * windows do not fit one LDS chunk buffer) */
+#define PDD_SWEEP_FACTOR_G2 4
+#define PDD_SWEEP_FACTOR_G4 8  /* groups of 4 channels only */
 int pdd_sweep_plan_create_ex(const int32_t* host_table, int64_t D, int64_t C, int dtype, int flags,
                              pdd_sweep_plan** plan);
-/* Channels per factor group of the plan (0 = channel by channel) and, if
+/* Channels per factor group of the plan (4 or 2; 0 = channel by channel) and, if
  * n_patterns is non-null, its stage-1 pattern count. */
 int pdd_sweep_plan_factor(const pdd_sweep_plan* plan, int64_t* n_patterns);
 /* x: [C][N] (ld) of the plan's dtype; out: [D][ld_out] float32.

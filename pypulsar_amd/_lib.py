@@ -27,6 +27,8 @@ ENOCHAIN = -5          # pdd_subband_chain: geometry does not chain (nothing lau
 ZDM_NONE, ZDM_INT, ZDM_WRAP = 0, 1, 2
 SWEEP_FACTOR = 1       # pdd_sweep_plan_create_ex: exact factorised 8-bit sweeps allowed
 SWEEP_FACTOR_FORCE = 2  # ... and taken whenever the windows fit (tests)
+SWEEP_FACTOR_G2 = 4     # ... over groups of 2 channels only
+SWEEP_FACTOR_G4 = 8     # ... over groups of 4 channels only
 
 # every symbol include/pdd.h declares (checked by tests/test_abi.py)
 EXPORTS = (

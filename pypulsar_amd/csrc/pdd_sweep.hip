@@ -642,8 +642,8 @@ __global__ __launch_bounds__(256) void k_interleave_u16_ds_v(const uint8_t* __re
 }
 
 // ------------------------------------------------------------------ factorised sweep
-// Exact factorisation of the 8-bit sweep over groups of FX = 4 adjacent
-// channels.  Within a group (channels c0..c0+3) trial d's shifts are its base
+// Exact factorisation of the 8-bit sweep over groups of fx = 4 (or 2)
+// adjacent channels.  Within a group (channels c0..c0+3) trial d's shifts are its base
 // shift b = table[d][c0] plus a RELATIVE pattern r = (0, r1, r2, r3); the
 // group's contribution to plane[d][t] is
 //     sum_k X(c0 + k, t + b + r_k) = S_r(t + b),  S_r(u) = sum_k X(c0 + k, u + r_k),
@@ -657,9 +657,8 @@ __global__ __launch_bounds__(256) void k_interleave_u16_ds_v(const uint8_t* __re
 // channel sweep, the same window staging (a tile stages every pattern its
 // trials use: 3.8 of a group's patterns per 48-trial block, 0.88 x the
 // channel windows' elements).
-constexpr int kFx = 4;
 __global__ __launch_bounds__(256) void k_fx_patterns(const uint4* __restrict__ R, int64_t nR,
-                                                     const int4* __restrict__ pat,
+                                                     const int4* __restrict__ pat, int fx,
                                                      uint4* __restrict__ P) {
   const int64_t p = blockIdx.x;
   const int4 q = pat[p];  // {c0, r1, r2, r3}
@@ -674,7 +673,9 @@ __global__ __launch_bounds__(256) void k_fx_patterns(const uint4* __restrict__ R
   for (int i = 0; i < kIlPer; ++i) {
     const int64_t j = j0 + i * 256;
     if (j >= nR) continue;
-    const uint4 a = at(0, 0, j), b = at(1, q.y, j), c = at(2, q.z, j), d = at(3, q.w, j);
+    const uint4 a = at(0, 0, j), b = at(1, q.y, j);
+    const uint4 c = fx > 2 ? at(2, q.z, j) : make_uint4(0u, 0u, 0u, 0u);
+    const uint4 d = fx > 3 ? at(3, q.w, j) : make_uint4(0u, 0u, 0u, 0u);
     v[i] = make_uint4(a.x + b.x + c.x + d.x, a.y + b.y + c.y + d.y, a.z + b.z + c.z + d.z,
                       a.w + b.w + c.w + d.w);
   }
@@ -696,16 +697,15 @@ constexpr int kFxE = 512, kFxRspan = 512;
 __global__ __launch_bounds__(256) void k_fx_patterns_lds(const uint4* __restrict__ R, int64_t nR,
                                                          const int4* __restrict__ pat,
                                                          const int* __restrict__ gtab, int NG,
-                                                         uint4* __restrict__ P) {
+                                                         int fx, uint4* __restrict__ P) {
   extern __shared__ __attribute__((aligned(16))) uint4 L[];
   const int g = blockIdx.x;
   const int64_t j0 = (int64_t)blockIdx.y * kFxE;
   const int p0 = gtab[g], p1 = gtab[g + 1];
   const int lo = gtab[NG + 1 + 2 * g], hi = gtab[NG + 2 + 2 * g];
   const int W = kFxE + hi - lo;
-  const uint4* r0 = R + (int64_t)(g * kFx) * nR;
-#pragma unroll
-  for (int k = 0; k < kFx; ++k)
+  const uint4* r0 = R + (int64_t)(g * fx) * nR;
+  for (int k = 0; k < fx; ++k)
     for (int e = threadIdx.x; e < W; e += 256) {
       const int64_t i = j0 + lo + e;
       L[k * W + e] = (i >= 0 && i < nR) ? r0[(int64_t)k * nR + i] : make_uint4(0u, 0u, 0u, 0u);
@@ -717,8 +717,9 @@ __global__ __launch_bounds__(256) void k_fx_patterns_lds(const uint4* __restrict
     for (int e = threadIdx.x; e < kFxE; e += 256) {
       const int64_t j = j0 + e;
       if (j >= nR) break;
-      const uint4 a = L[e - lo], b = L[W + e - lo + q.y], c = L[2 * W + e - lo + q.z],
-                  d = L[3 * W + e - lo + q.w];
+      const uint4 a = L[e - lo], b = L[W + e - lo + q.y];
+      const uint4 c = fx > 2 ? L[2 * W + e - lo + q.z] : make_uint4(0u, 0u, 0u, 0u);
+      const uint4 d = fx > 3 ? L[3 * W + e - lo + q.w] : make_uint4(0u, 0u, 0u, 0u);
       P[(int64_t)p * nR + j] = make_uint4(a.x + b.x + c.x + d.x, a.y + b.y + c.y + d.y,
                                           a.z + b.z + c.z + d.z, a.w + b.w + c.w + d.w);
     }
@@ -744,6 +745,40 @@ __device__ __forceinline__ int stage_il_dma(uint32_t lds_dst, const float4* src,
   }
   return first < nq ? (nq - 1 - first) / step + 1 : 0;
 }
+
+// A whole window from ONE wave: runs of up to four consecutive 1 KiB DMAs
+// share one M0 value, the instruction offset (0 / 1024 / 2048 / 3072 bytes)
+// moving both the global source and the LDS destination
+// (scripts/probes/dma_offset.hip checks the LDS side on the device).
+__device__ __forceinline__ int stage_il_dma_win(uint32_t lds_dst, const float4* src, int ne,
+                                                int lane) {
+  const int nq = (ne + 63) >> 6;
+  for (int q = 0; q < nq; q += 4) {
+    const float4* s = src + q * 64 + lane;
+    const uint32_t m = __builtin_amdgcn_readfirstlane(lds_dst + q * 1024);
+    uint32_t keep;
+    switch (min(4, nq - q)) {
+#define PDD_DMA_RUN(TEXT)                                                                      \
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t" TEXT "s_mov_b32 m0, %0" \
+               : "=&s"(keep) : "v"(s), "s"(m) : "memory")
+      case 1: PDD_DMA_RUN("global_load_lds_dwordx4 %1, off\n\t"); break;
+      case 2: PDD_DMA_RUN("global_load_lds_dwordx4 %1, off\n\t"
+                          "global_load_lds_dwordx4 %1, off offset:1024\n\t"); break;
+      case 3: PDD_DMA_RUN("global_load_lds_dwordx4 %1, off\n\t"
+                          "global_load_lds_dwordx4 %1, off offset:1024\n\t"
+                          "global_load_lds_dwordx4 %1, off offset:2048\n\t"); break;
+      default: PDD_DMA_RUN("global_load_lds_dwordx4 %1, off\n\t"
+                           "global_load_lds_dwordx4 %1, off offset:1024\n\t"
+                           "global_load_lds_dwordx4 %1, off offset:2048\n\t"
+                           "global_load_lds_dwordx4 %1, off offset:3072\n\t"); break;
+#undef PDD_DMA_RUN
+    }
+  }
+  return nq;
+}
+#ifndef PDD_IL_DMA_WIN
+#define PDD_IL_DMA_WIN 1
+#endif
 
 // Synchronisation of k_sweep_il: one s_barrier per chunk.  Before barrier k
 // the loader waves retire chunk k's DMAs with a counted vmcnt (chunks k+1 ..
@@ -928,8 +963,15 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       const int len = __builtin_amdgcn_readlane(rec.y, i);
       const int off = __builtin_amdgcn_readlane(rec.z, i);
       const int row = __builtin_amdgcn_readlane(rec.w, i) & 0xfffff;
-      n += stage_il_dma(img_lds + (uint32_t)((b * buf_e + off) * 16),
-                        R + (int64_t)row * nR + (t0 + bm - lo), len, first, step, lane);
+      if (PDD_IL_DMA_WIN) {
+        // window i from loader i mod NLW, its DMAs in runs sharing M0
+        if (i % step == first)
+          n += stage_il_dma_win(img_lds + (uint32_t)((b * buf_e + off) * 16),
+                                R + (int64_t)row * nR + (t0 + bm - lo), len, lane);
+      } else {
+        n += stage_il_dma(img_lds + (uint32_t)((b * buf_e + off) * 16),
+                          R + (int64_t)row * nR + (t0 + bm - lo), len, first, step, lane);
+      }
     }
     return n;
   };
@@ -990,9 +1032,16 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
 #pragma unroll
       for (int i = 0; i < CC; ++i) {
         if (i >= ncc) break;
-        n += stage_il_dma(img_lds + (uint32_t)((b * buf_e + rr[i].z) * 16),
-                          R + (int64_t)(rr[i].w & 0xfffff) * nR + (t0 + rr[i].x - lo), Tq + rr[i].y,
-                          lw, NLW, lane);
+        if (PDD_IL_DMA_WIN) {
+          if (i % NLW == lw)
+            n += stage_il_dma_win(img_lds + (uint32_t)((b * buf_e + rr[i].z) * 16),
+                                  R + (int64_t)(rr[i].w & 0xfffff) * nR + (t0 + rr[i].x - lo),
+                                  Tq + rr[i].y, lane);
+        } else {
+          n += stage_il_dma(img_lds + (uint32_t)((b * buf_e + rr[i].z) * 16),
+                            R + (int64_t)(rr[i].w & 0xfffff) * nR + (t0 + rr[i].x - lo), Tq + rr[i].y,
+                            lw, NLW, lane);
+        }
       }
       return n;
     };
@@ -1586,11 +1635,11 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
       if (p->d_gtab) {
         const int NG = (int)(p->C / p->fx);
         hipLaunchKernelGGL(k_fx_patterns_lds, dim3((unsigned)NG, (unsigned)cdiv(nR, kFxE)), dim3(256),
-                           (size_t)(kFx * (kFxE + kFxRspan)) * sizeof(uint4), st, (const uint4*)R, nR,
-                           (const int4*)p->d_pat, p->d_gtab, NG, P);
+                           (size_t)(p->fx * (kFxE + kFxRspan)) * sizeof(uint4), st, (const uint4*)R, nR,
+                           (const int4*)p->d_pat, p->d_gtab, NG, p->fx, P);
       } else {
         hipLaunchKernelGGL(k_fx_patterns, dim3((unsigned)p->n_pat, (unsigned)cdiv(nR, 256 * kIlPer)),
-                           dim3(256), 0, st, (const uint4*)R, nR, (const int4*)p->d_pat, P);
+                           dim3(256), 0, st, (const uint4*)R, nR, (const int4*)p->d_pat, p->fx, P);
       }
       if (hipGetLastError() != hipSuccess) { rc = -3; break; }
     }
@@ -1634,9 +1683,9 @@ struct FxTables {
   double cost_b = 0, cost_f = 0;   // modelled cycles per time tile: channel sweep / factorised
 };
 static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v, int64_t buf_e,
-                     bool force, FxTables& T) {
-  if (C % kFx != 0 || C < 2 * kFx) return false;
-  const int64_t NG = C / kFx, DB = v.DB(), ROW = DB + 4, Tq = 64 * v.G;
+                     int fx, bool force, FxTables& T) {
+  if (C % fx != 0 || C < 2 * fx) return false;
+  const int64_t NG = C / fx, DB = v.DB(), ROW = DB + 4, Tq = 64 * v.G;
   const int64_t n_dblk = cdiv(D, DB);
   // pattern of (trial, group): relative shifts r1..r3 (packed key) -> pool row
   std::vector<int> pid((size_t)(D * NG));
@@ -1645,9 +1694,9 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
   for (int64_t g = 0; g < NG; ++g) {
     idx.clear();
     for (int64_t d = 0; d < D; ++d) {
-      const int32_t* r = tab + d * C + g * kFx;
+      const int32_t* r = tab + d * C + g * fx;
       uint64_t key = 0;
-      for (int k = 1; k < kFx; ++k) {
+      for (int k = 1; k < fx; ++k) {
         const int64_t rel = (int64_t)r[k] - r[0];
         if (rel < -(1 << 20) || rel >= (1 << 20)) return false;
         key = (key << 21) | (uint64_t)(rel + (1 << 20));
@@ -1657,8 +1706,8 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
       if (it == idx.end()) {
         id = (int)(T.pat.size() / 4);
         idx.emplace(key, id);
-        T.pat.push_back((int)(g * kFx));
-        for (int k = 1; k < kFx; ++k) T.pat.push_back(r[k] - r[0]);
+        T.pat.push_back((int)(g * fx));
+        for (int k = 1; k < 4; ++k) T.pat.push_back(k < fx ? r[k] - r[0] : 0);
       } else {
         id = it->second;
       }
@@ -1672,11 +1721,11 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
     bool fits = true;
     int64_t g = -1;
     for (int64_t p = 0; p < T.n_pat; ++p) {
-      const int64_t pg = T.pat[(size_t)(4 * p)] / kFx;
+      const int64_t pg = T.pat[(size_t)(4 * p)] / fx;
       while (g < pg) T.gtab[(size_t)(++g)] = (int)p;
       int& lo = T.gtab[(size_t)(NG + 1 + 2 * pg)];
       int& hi = T.gtab[(size_t)(NG + 2 + 2 * pg)];
-      for (int k = 1; k < kFx; ++k) {
+      for (int k = 1; k < fx; ++k) {
         lo = std::min(lo, T.pat[(size_t)(4 * p + k)]);
         hi = std::max(hi, T.pat[(size_t)(4 * p + k)]);
       }
@@ -1686,7 +1735,7 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
     if (!fits) T.gtab.clear();
   }
   // (a quick screen: stage 1 + stage 2 adds against the channel sweep's)
-  if (!force && (double)T.n_pat * kFx + (double)D * NG > 0.5 * (double)D * C) return false;
+  if (!force && (double)T.n_pat * fx + (double)D * NG > 0.75 * (double)D * C) return false;
   if (T.n_pat + 1 >= (1 << 20)) return false;
   const int zero_row = (int)T.n_pat;  // pad groups read a window of this row of zeros
   // Rows (metadata) are laid out per trial block in chunk order: the groups,
@@ -1724,7 +1773,7 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
       for (int64_t j = 0; j < DB; ++j) {
         const int64_t d = std::min(b * DB + j, D - 1);
         const int id = pid[(size_t)(d * NG + g)];
-        const int base = tab[d * C + g * kFx];
+        const int base = tab[d * C + g * fx];
         size_t i = 0;
         while (i < w.size() && w[i][0] != id) ++i;
         if (i == w.size()) w.push_back({id, base, base});
@@ -1755,7 +1804,7 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
         if (g >= 0 && g < NG) {
           const int64_t d = std::min(b * DB + j, D - 1);
           const int id = pid[(size_t)(d * NG + g)];
-          const int base = tab[d * C + g * kFx];
+          const int base = tab[d * C + g * fx];
           size_t i = 0;
           while (w[i][0] != id) ++i;
           o = (int)(16 * (off[i] + base - w[i][1]));
@@ -1792,8 +1841,8 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
     // sweep's compute waves take ~440 cycles per channel and its loaders
     // ~1.15 per staged element (LDS-DMA issue), with ~15% synchronisation
     // (2.06 M cycles per configs[3] tile); the factorised stage 2 has a
-    // quarter of the compute and is loader-bound at ~1.44 x its staging
-    // (1.37 M cycles per configs[3] tile)
+    // quarter of the compute and is loader-bound at ~1.16 x its staging
+    // (1.10 M cycles per configs[3] tile, window DMAs in M0-sharing runs)
     int64_t el_b = 0, el_f = 0;  // staged elements: channel sweep / factorised
     for (int64_t c = 0; c < C; ++c) {
       int lo_ = INT32_MAX, hi_ = INT32_MIN;
@@ -1807,7 +1856,7 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
     for (const auto& ch : cw[(size_t)b])
       for (const auto& r : ch) el_f += (r[1] + 63) / 64 * 64;
     cost_b += 1.15 * std::max(440.0 * (double)C, 1.15 * (double)el_b);
-    cost_f += 1.44 * std::max(110.0 * (double)C, 1.15 * (double)el_f);
+    cost_f += 1.16 * std::max(110.0 * (double)C, 1.15 * (double)el_f);
   }
   // stage 1 per time tile: every pattern's 2 KiB of eighths, written once
   // for all trial blocks at ~6.7 B per CU cycle (k_fx_patterns_lds: 4.1 TB/s)
@@ -2034,11 +2083,23 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
       }
       p->maxch = (int)maxch;
       // 8-bit single-group sweeps: the factorised tables when they pay
-      FxTables T;
+      // groups of 4 channels, or of 2 where 4 do not fit or pay (the
+      // cheaper by the cost model; PDD_SWEEP_FACTOR_G2 / _G4: that size only)
+      FxTables T, T2;
+      const bool force = (flags & PDD_SWEEP_FACTOR_FORCE) != 0;
+      int fxg = 0;
       if ((flags & PDD_SWEEP_FACTOR) && dtype == PDD_U8 && n_grp == 1 && v.S == 8 &&
-          il_kernel_for(v, true) &&
-          fx_build(host_table, D, C, v, buf_e, (flags & PDD_SWEEP_FACTOR_FORCE) != 0, T)) {
-        p->fx = kFx;
+          il_kernel_for(v, true)) {
+        if (!(flags & PDD_SWEEP_FACTOR_G2) && fx_build(host_table, D, C, v, buf_e, 4, force, T))
+          fxg = 4;
+        if (!(flags & PDD_SWEEP_FACTOR_G4) && fx_build(host_table, D, C, v, buf_e, 2, force, T2) &&
+            (fxg == 0 || T2.cost_f < T.cost_f)) {
+          fxg = 2;
+          std::swap(T, T2);
+        }
+      }
+      if (fxg) {
+        p->fx = fxg;
         p->n_pat = T.n_pat;
         p->fx_rows = T.rows_pb;
         p->maxch = T.maxch;
@@ -2056,7 +2117,7 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
         if (e == hipSuccess && !T.gtab.empty())
           e = hipFuncSetAttribute((const void*)k_fx_patterns_lds,
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)(kFx * (kFxE + kFxRspan) * sizeof(uint4)));
+                                  (int)(4 * (kFxE + kFxRspan) * sizeof(uint4)));
         if (e != hipSuccess) {
           set_error("pdd_sweep_plan_create: %s", hipGetErrorString(e));
           pdd_sweep_plan_destroy(p);

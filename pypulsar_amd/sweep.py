@@ -65,8 +65,9 @@ class DMSweep(object):
         often (pdd_sweep_plan_set_input_max).  ``factor``: 8-bit plans may
         sweep exactly factorised over groups of 4 channels when that pays
         (pdd_sweep_plan_create_ex PDD_SWEEP_FACTOR; bit-identical planes);
-        False forces the channel-by-channel kernel; "force" factorises even
-        where it does not pay (tests of small grids)."""
+        False forces the channel-by-channel kernel; 2 or 4: that group size
+        only (still where it pays); "force2" / "force4" (= "force"): that
+        group size wherever the windows fit, paying or not (tests)."""
         _lib.require_gpu()
         self.dms = np.atleast_1d(np.asarray(dms, dtype=np.float64))
         self.freqs = np.asarray(freqs, dtype=np.float64)
@@ -79,7 +80,10 @@ class DMSweep(object):
         self.max_bin = int(self.table.max()) if self.table.size else 0
         self.dtype = dtype
         self.input_max = None if input_max is None else int(input_max)
-        self.factor = factor if factor == "force" else bool(factor)
+        if factor == "force":
+            factor = "force4"
+        assert factor in (True, False, 2, 4, "force2", "force4"), "bad factor %r" % (factor,)
+        self.factor = factor
         if self.input_max is not None:
             assert dtype in ("u8", "u16") and 1 <= self.input_max <= (255 if dtype == "u8" else 1023)
         self._plans = {}
@@ -91,8 +95,7 @@ class DMSweep(object):
             tab = np.ascontiguousarray(self.table)
             _lib.check(_lib.lib().pdd_sweep_plan_create_ex(
                 tab.ctypes.data_as(ctypes.c_void_p), self.D, self.C, code,
-                (_lib.SWEEP_FACTOR | _lib.SWEEP_FACTOR_FORCE) if self.factor == "force"
-                else (_lib.SWEEP_FACTOR if self.factor else 0), ctypes.byref(h)),
+                self._factor_flags(), ctypes.byref(h)),
                 "pdd_sweep_plan_create_ex")
             p = h
             self._plans[code] = p
@@ -108,6 +111,18 @@ class DMSweep(object):
         keys = ("D", "C", "dms_per_block", "samples_per_block", "lds_bytes", "max_bin", "min_bin",
                 "variant")
         return dict(zip(keys, (int(v) for v in a)))
+
+    def _factor_flags(self):
+        f = self.factor
+        if f is False:
+            return 0
+        flags = _lib.SWEEP_FACTOR
+        if isinstance(f, str):
+            flags |= _lib.SWEEP_FACTOR_FORCE
+            f = int(f[-1])
+        if f is not True:
+            flags |= _lib.SWEEP_FACTOR_G2 if f == 2 else _lib.SWEEP_FACTOR_G4
+        return flags
 
     def factor_info(self, code=_lib.U8):
         """(channels per factor group, stage-1 patterns) of the plan for

@@ -16,7 +16,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "gpurun_out", "final3", "prof")
+SRC = os.path.join(ROOT, "gpurun_out", os.environ.get("FINAL", "final3"), "prof")
 DST = os.path.join(ROOT, "profiles")
 TAG = sys.argv[1] if len(sys.argv) > 1 else "r3final"
 ARGS = {"config3": "--config config3", "config2_u8": "--config config2 --dtype u8",

@@ -7,7 +7,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp PYTHONDONTWRITEBYTECODE=1
-O=gpurun_out/final3
+O=${O:-gpurun_out/final3}
 mkdir -p $O
 PARTS=${PARTS:-"tests bench prof"}
 run() { local t=$1 n=$2; shift 2; timeout -k 10 $t "$@" > $O/$n.json 2> $O/$n.err || { echo "FAIL $n"; tail -5 $O/$n.err; exit 1; }; echo "$n: $(cut -c1-200 $O/$n.json)"; }
@@ -19,6 +19,7 @@ tests)
   tail -1 $O/pytest_gpu.log ;;
 bench)
   run 900 bench_config3 python bench.py
+  run 600 bench_config3_channel python bench.py --factor off --no-cpu-baseline --no-e2e
   run 300 bench_config2_f32 python bench.py --config config2 --no-cpu-baseline
   run 300 bench_config2_u8 python bench.py --config config2 --dtype u8 --no-cpu-baseline
   run 600 bench_northstar python bench.py --config northstar --no-cpu-baseline --no-e2e

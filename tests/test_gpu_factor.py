@@ -17,11 +17,12 @@ DT = 64e-6
 @pytest.mark.gpu
 @pytest.mark.parametrize("pad", [0, 7, "rotate"])
 @pytest.mark.parametrize("descending", [True, False])
-@pytest.mark.parametrize("C", [32, 36])
-def test_factor_small_grids_vs_oracle(gpu, pad, descending, C):
-    """Forced factorisation on small grids: pads (value / rotate) past the
-    block edge (trim=False), ascending bands (negative relative shifts), an
-    odd group count (C = 36: 9 groups, the last pair ends in a zero group)."""
+@pytest.mark.parametrize("C,g", [(32, 4), (36, 4), (36, 2), (34, 2)])
+def test_factor_small_grids_vs_oracle(gpu, pad, descending, C, g):
+    """Forced factorisation on small grids, groups of 4 and of 2 channels:
+    pads (value / rotate) past the block edge (trim=False), ascending bands
+    (negative relative shifts), odd group counts (C = 36 in 4s: 9 groups; C =
+    34 in 2s: 17 groups -- the last pair ends in a zero group)."""
     import torch
     from pypulsar_amd.sweep import DMSweep
     N, D = 6000, 64
@@ -30,8 +31,8 @@ def test_factor_small_grids_vs_oracle(gpu, pad, descending, C):
     # (a grid whose group pairs' pattern windows fit one chunk buffer: with
     # 9-MHz channels every trial of a wider grid has its own pattern)
     dms = np.linspace(0, 3.0 if C == 32 else 4.0, D)
-    sw = DMSweep(dms, freqs, DT, dtype="u8", factor="force")
-    assert sw.factor_info()[0] == 4
+    sw = DMSweep(dms, freqs, DT, dtype="u8", factor="force" if g == 4 else "force2")
+    assert sw.factor_info()[0] == g
     for trim in (True, False):
         plane = sw(torch.from_numpy(x).cuda(), padval=pad, trim=trim).cpu().numpy()
         tab = orc.sweep_table(dms, freqs, DT)
