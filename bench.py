@@ -472,7 +472,7 @@ def sweep_bench(args, cfg, rank, world, dev):
     # exact factorised 8-bit sweep: the kernel adds one
     # pattern sample per (trial, group of fx channels), so its own adds are
     # C / fx per samp*DM; the algorithmic rate is reported beside them
-    fx_g, fx_pat = sw.factor_info() if (sw is not None and dtype == "u8") else (0, 0)
+    fx_g, fx_pat = sw.factor_info(1) if (sw is not None and dtype == "u8") else (0, 0)
     kern_adds_step = rows * n_out * (C // fx_g) if fx_g else adds_rank_step
     achieved = kern_adds_step * steps / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else None
     effective = adds_rank_step * steps / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else None
@@ -485,7 +485,13 @@ def sweep_bench(args, cfg, rank, world, dev):
     valu_roof = VALU_LANE_OPS_T * valu_adds
     uniq_bytes = C * N * s_in + rows * n_out * 4
     k_s = kern_ms * 1e-3 / steps if kern_ms > 0 else None
+    # keys of profiles/pmc_sweep.json (scripts/collect_profiles_r3.py): the
+    # default configs[3] line (factorised), its channel-kernel line, ...
     pmc_key = "%s_%s" % (args.config, dtype)
+    if args.config == "config3" and not fx_g:
+        pmc_key = "config3_channel"
+    elif args.config == "northstar":
+        pmc_key = "northstar"
     pmc = load_pmc(os.path.join(ROOT, "profiles", "pmc_sweep.json"), pmc_key)
     traffic = pmc.get("hbm_bytes_per_launch") if isinstance(pmc, dict) else None
 
@@ -928,6 +934,8 @@ def stream_bench(args, cfg, rank, world, dev):
     lds_roof = N_CU * CLK_GHZ * 1e9 * LDS_B_PER_CLK / 16 * (8 if st.exact else 4) / 1e12
     ms = el / args.steps * 1e3
     in_rate = block * args.steps * world / el  # input spectra per second
+    fx_g, fx_pat = st.sweep.factor_info(2 if st.exact else 0) if st.exact else (0, 0)
+    h2d_bytes = block * C  # one 8-bit block per step over PCIe (pinned, async)
     line = {
         "metric": "DM-trial samples*channels/sec (node) + % HBM roofline",
         "value": value, "unit": "samples*channels*DM/s (downsampled samples)",
@@ -946,7 +954,11 @@ def stream_bench(args, cfg, rank, world, dev):
                                          "float": "x - mean in float32 (the reference's float "
                                                   "data semantics)",
                                          "none": "no filter"}[st.mode],
-                   "u16_flush_channels": (min(256, 65535 // st.input_max) if st.exact else None),
+                   "u16_flush_channels": (min(256, 65535 // (st.input_max * max(1, fx_g)))
+                                          if st.exact else None),
+                   "method": ("exact factorisation over groups of %d channels (%d pattern "
+                              "series; plane bit-identical)" % (fx_g, fx_pat) if fx_g
+                              else "channel by channel"),
                    "config_name": "stream", "channels": C, "block": block, "overlap": st.ov,
                    "downsamp": ds, "dm_trials": D, "parallelism": "tb%d" % world},
         "realtime_factor": (block * dt) / (ms * 1e-3),
@@ -955,8 +967,13 @@ def stream_bench(args, cfg, rank, world, dev):
                      "peak": lds_roof, "unit": "T adds/s",
                      "frac": D * nb * C / (ms * 1e-3) / 1e12 / lds_roof, "traffic": None,
                      "note": "whole-step time (H2D, prologue, sweep) per block; one add per "
-                             "unit against the sweep's LDS read roof (%s image)"
-                             % ("u16 eighths" if st.exact else "float32 quarters")},
+                             "unit against the sweep's LDS read roof (%s image)%s"
+                             % ("u16 eighths" if st.exact else "float32 quarters",
+                                "; factorised: the sweep adds 1/%d of these and the step is "
+                                "bound by the block's H2D (h2d_GBs_at_step)" % fx_g if fx_g
+                                else "")},
+        "h2d_bytes_per_step": h2d_bytes,
+        "h2d_GBs_at_step": h2d_bytes / (ms * 1e-3) / 1e9,
         "cpu_baseline": None,
     }
     st.close()

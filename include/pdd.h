@@ -177,8 +177,9 @@ typedef struct pdd_sweep_plan pdd_sweep_plan;
 int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int dtype,
                           pdd_sweep_plan** plan);
 /* The same with plan flags (pdd_sweep_plan_create = PDD_SWEEP_FACTOR):
- * PDD_SWEEP_FACTOR lets an 8-bit plan (C a multiple of 4) sweep EXACTLY
- * factorised over groups of 4 adjacent channels when that pays: each
+ * PDD_SWEEP_FACTOR lets an integer plan (PDD_U8 / PDD_U16, single group)
+ * sweep EXACTLY factorised over groups of 4 (or 2) adjacent channels when
+ * that pays: each
  * group's distinct relative-shift patterns are summed once (stage 1), and
  * every trial adds its pattern series at the group's base shift (stage 2) --
  * the same integer samples as the channel-by-channel sum, so the plane is

@@ -1571,8 +1571,8 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
   // factorised plans: the pattern image (stage 1), n_pat rows + a row of zeros
   uint4* P = nullptr;
   if (p->fx) {
-    PDD_REQUIRE(u16 && p->dtype == PDD_U8 && ds == 1 && !ex.r2_pad && !ex.R_pre && p->n_grp == 1,
-                "pdd_sweep_execute: factorised plans take 8-bit input at the raw rate");
+    PDD_REQUIRE(u16 && p->dtype != PDD_F32 && ds == 1 && !ex.r2_pad && !ex.R_pre && p->n_grp == 1,
+                "pdd_sweep_execute: factorised plans take 8/16-bit input at the raw rate");
     P = static_cast<uint4*>(scratch(st, kScratchPattern, (size_t)((p->n_pat + 1) * nr_alloc) * sizeof(uint4)));
     if (!P) return -2;
   }
@@ -2082,13 +2082,13 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
         for (size_t k = 0; k < chunks[i].size(); ++k) bmin[i * (maxch + 1) + 1 + k] = chunks[i][k];
       }
       p->maxch = (int)maxch;
-      // 8-bit single-group sweeps: the factorised tables when they pay
+      // 8/16-bit single-group sweeps: the factorised tables when they pay
       // groups of 4 channels, or of 2 where 4 do not fit or pay (the
       // cheaper by the cost model; PDD_SWEEP_FACTOR_G2 / _G4: that size only)
       FxTables T, T2;
       const bool force = (flags & PDD_SWEEP_FACTOR_FORCE) != 0;
       int fxg = 0;
-      if ((flags & PDD_SWEEP_FACTOR) && dtype == PDD_U8 && n_grp == 1 && v.S == 8 &&
+      if ((flags & PDD_SWEEP_FACTOR) && dtype != PDD_F32 && n_grp == 1 && v.S == 8 &&
           il_kernel_for(v, true)) {
         if (!(flags & PDD_SWEEP_FACTOR_G2) && fx_build(host_table, D, C, v, buf_e, 4, force, T))
           fxg = 4;

@@ -19,7 +19,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "gpurun_out", os.environ.get("FINAL", "final3"), "prof")
 DST = os.path.join(ROOT, "profiles")
 TAG = sys.argv[1] if len(sys.argv) > 1 else "r3final"
-ARGS = {"config3": "--config config3", "config2_u8": "--config config2 --dtype u8",
+ARGS = {"config3": "--config config3", "config3_channel": "--config config3 --factor off",
+        "northstar": "--config northstar", "config2_u8": "--config config2 --dtype u8",
         "config2_f32": "--config config2 --dtype f32", "stream": "--config stream"}
 
 
@@ -41,6 +42,15 @@ def main():
             shutil.copy(f[0], os.path.join(DST, "%s_%s_kernel_stats.csv" % (TAG, name)))
         fe = per_kernel(os.path.join(SRC, "fe_" + name, "**", "*counter_collection.csv"), "FETCH_SIZE")
         wr = per_kernel(os.path.join(SRC, "wr_" + name, "**", "*counter_collection.csv"), "WRITE_SIZE")
+        # factorised plans: the stage-1 pattern kernel's traffic beside the sweep's
+        for n1 in fe:
+            if "k_fx_patterns" in n1:
+                key1 = ("config3_u8" if name == "config3" else name) + "_stage1"
+                pmc[key1] = {"kernel": n1, "fetch_size_kb_per_launch": fe[n1][0],
+                             "write_size_kb_per_launch": wr.get(n1, (0.0, 0))[0],
+                             "launches": fe[n1][1],
+                             "hbm_bytes_per_launch": 2 * fe[n1][0] * 1024 + wr.get(n1, (0.0, 0))[0] * 1024,
+                             "round": TAG}
         k = [n for n in fe if "k_sweep" in n]
         if not k:
             continue

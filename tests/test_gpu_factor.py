@@ -119,3 +119,28 @@ def test_factor_chosen_for_config3_grid(gpu):
     g, n_pat = sw.factor_info()
     assert g == 4 and n_pat > 1024
     sw.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("input_max", [None, 510])
+def test_factor_16bit_input_vs_oracle(gpu, input_max):
+    """16-bit input (samples <= 1023: the offset zero-DM + downsample image of
+    the stream; <= 510 for its uint8-wrap mode, input_max) factorised in
+    groups of 4 and of 2: pattern sums <= 4 x 1023 stay exact in the packed
+    u16 lanes, which flush every floor(65535 / (g x max)) groups."""
+    import torch
+    from pypulsar_amd.sweep import DMSweep
+    C, N, D = 36, 6000, 64
+    freqs = band(C)
+    vmax = 1023 if input_max is None else input_max
+    rng = np.random.default_rng(7)
+    x = rng.integers(0, vmax + 1, size=(C, N)).astype(np.int16)
+    dms = np.linspace(0, 4.0, D)
+    tab = orc.sweep_table(dms, freqs, DT)
+    want = orc.sweep_plane(x.astype(np.float64), tab, 0)
+    for mode, g in (("force4", 4), ("force2", 2)):
+        sw = DMSweep(dms, freqs, DT, dtype="u16", input_max=input_max, factor=mode)
+        assert sw.factor_info(2)[0] == g
+        plane = sw(torch.from_numpy(x).cuda()).cpu().numpy().astype(np.float64)
+        np.testing.assert_array_equal(plane, want, err_msg="g %d" % g)
+        sw.close()
