@@ -39,8 +39,9 @@ static void hip_ok(hipError_t e, const char* what) {
 }
 
 // one sweep of a random [C][N] 8-bit block over a random table, f32 or u8
+static int factorised_cases = 0;
 static void sweep_case(std::mt19937& rng, int64_t C, int64_t N, int64_t D, int span, int dtype,
-                       bool timing) {
+                       bool timing, int flags = PDD_SWEEP_FACTOR) {
   std::vector<int32_t> tab((size_t)(D * C));
   std::uniform_int_distribution<int> sh(0, span);
   for (int64_t d = 0; d < D; ++d)
@@ -54,10 +55,15 @@ static void sweep_case(std::mt19937& rng, int64_t C, int64_t N, int64_t D, int s
   std::vector<float> xf(x8.begin(), x8.end());
 
   pdd_sweep_plan* plan = nullptr;
-  int rc = pdd_sweep_plan_create(tab.data(), D, C, dtype, &plan);
+  int rc = pdd_sweep_plan_create_ex(tab.data(), D, C, dtype, flags, &plan);
   CHECK(rc == 0 && plan, "plan_create C=%lld D=%lld span=%d dtype=%d: rc=%d %s", (long long)C,
         (long long)D, span, dtype, rc, pdd_last_error());
   if (rc != 0) return;
+  int64_t n_pat = -1;
+  const int fx = pdd_sweep_plan_factor(plan, &n_pat);
+  CHECK(fx == 0 || ((fx == 2 || fx == 4) && C % fx == 0 && n_pat > 0 && dtype != PDD_F32),
+        "factor %d (%lld patterns) for C=%lld dtype=%d", fx, (long long)n_pat, (long long)C, dtype);
+  if (fx) ++factorised_cases;
   int64_t info[8] = {0};
   CHECK(pdd_sweep_plan_info(plan, info) == 0 && info[0] == D && info[1] == C, "plan_info");
   if (timing) CHECK(pdd_sweep_set_timing(plan, 1) == 0, "set_timing");
@@ -267,6 +273,20 @@ int main() {
             ++cases;
           }
 
+  // forced exact factorisation (groups of 4 / of 2 channels) on random
+  // grids: the plan takes it wherever the windows fit, planes vs host sums
+  const int before = factorised_cases;
+  for (int64_t C : {8, 12, 64, 96})
+    for (int64_t D : {5, 57, 130})
+      for (int span : {0, 40, 300})
+        for (int fl : {PDD_SWEEP_FACTOR | PDD_SWEEP_FACTOR_FORCE,
+                       PDD_SWEEP_FACTOR | PDD_SWEEP_FACTOR_FORCE | PDD_SWEEP_FACTOR_G2}) {
+          sweep_case(rng, C, 3000, D, span, PDD_U8, (D & 1) != 0, fl);
+          ++cases;
+        }
+  CHECK(factorised_cases - before >= 24, "only %d forced grids factorised",
+        factorised_cases - before);
+
   // single-DM ops interleaved with more sweeps (shared per-stream scratch)
   int ops = 0;
   for (int64_t C : {16, 64, 2048})
@@ -286,6 +306,7 @@ int main() {
     CHECK(rc == 0 && q, "grouped create rep %d: %s", rep, pdd_last_error());
     if (q) CHECK(pdd_sweep_plan_destroy(q) == 0, "grouped destroy");
   }
-  std::printf("abi_asan: %d sweep cases, %d op cases, %d failures\n", cases, ops, failures);
+  std::printf("abi_asan: %d sweep cases (%d factorised), %d op cases, %d failures\n", cases,
+              factorised_cases, ops, failures);
   return failures ? 1 : 0;
 }
