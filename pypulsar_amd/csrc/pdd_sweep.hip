@@ -1475,6 +1475,7 @@ struct pdd_sweep_plan {
   int fx = 0;              // factorised sweep: channels per group (0 = channel by channel)
   int64_t n_pat = 0;       // factorised: pattern series (stage-1 rows, + 1 zero row)
   int64_t fx_rows = 0;     // factorised: metadata rows per trial block (groups + pad groups)
+  int fx_rspan = 0;        // factorised: widest relative-shift range of a group (stage-1 LDS)
   int* d_pat = nullptr;    // factorised: [n_pat][4] {c0, r1, r2, r3}
   int* d_wt = nullptr;     // factorised: [n_dblk][maxch][kFxWin][4] window records
   int* d_gtab = nullptr;   // factorised: per group first pattern + relative-shift range (LDS stage 1)
@@ -1635,7 +1636,7 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
       if (p->d_gtab) {
         const int NG = (int)(p->C / p->fx);
         hipLaunchKernelGGL(k_fx_patterns_lds, dim3((unsigned)NG, (unsigned)cdiv(nR, kFxE)), dim3(256),
-                           (size_t)(p->fx * (kFxE + kFxRspan)) * sizeof(uint4), st, (const uint4*)R, nR,
+                           (size_t)(p->fx * (kFxE + p->fx_rspan)) * sizeof(uint4), st, (const uint4*)R, nR,
                            (const int4*)p->d_pat, p->d_gtab, NG, p->fx, P);
       } else {
         hipLaunchKernelGGL(k_fx_patterns, dim3((unsigned)p->n_pat, (unsigned)cdiv(nR, 256 * kIlPer)),
@@ -1679,6 +1680,7 @@ extern "C" {
 struct FxTables {
   std::vector<int> pat, mt, cht, wt, gtab;  // gtab empty: a group's shift range exceeds kFxRspan
   int64_t n_pat = 0, rows_pb = 0;  // metadata rows per trial block
+  int rspan = 0;                   // widest relative-shift range of a group
   int maxch = 0;
   double cost_b = 0, cost_f = 0;   // modelled cycles per time tile: channel sweep / factorised
 };
@@ -1730,6 +1732,7 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
         hi = std::max(hi, T.pat[(size_t)(4 * p + k)]);
       }
       if (hi - lo > kFxRspan) fits = false;
+      T.rspan = std::max(T.rspan, hi - lo);
     }
     while (g < NG) T.gtab[(size_t)(++g)] = (int)T.n_pat;
     if (!fits) T.gtab.clear();
@@ -2102,6 +2105,7 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
         p->fx = fxg;
         p->n_pat = T.n_pat;
         p->fx_rows = T.rows_pb;
+        p->fx_rspan = T.rspan;  // stage 1 sizes its LDS to it: more workgroups per CU
         p->maxch = T.maxch;
         tab.swap(T.mt);
         bmin.swap(T.cht);
