@@ -23,6 +23,7 @@ bench)
   run 300 bench_config2_f32 python bench.py --config config2 --no-cpu-baseline
   run 300 bench_config2_u8 python bench.py --config config2 --dtype u8 --no-cpu-baseline
   run 600 bench_northstar python bench.py --config northstar --no-cpu-baseline --no-e2e
+  run 600 bench_northstar_channel python bench.py --config northstar --factor off --no-cpu-baseline --no-e2e
   run 300 bench_stream_wrap python bench.py --config stream --zdm wrap
   run 300 bench_stream_int python bench.py --config stream --zdm int
   run 300 bench_subband python bench.py --config subband
