@@ -726,6 +726,61 @@ __global__ __launch_bounds__(256) void k_fx_patterns_lds(const uint4* __restrict
   }
 }
 
+// Stage 1 straight from the input (no u16-eighths image R in HBM): the
+// load phase builds each of the group's row elements the way
+// k_interleave_u16 would -- 8 samples X(c, base + i + m*Qs), m < 8, as packed
+// u16 pairs, with the reference pads (value / rotate) -- then writes every
+// pattern of the group as k_fx_patterns_lds does.  Saves the image's write
+// and read, and the interleave launch, per segment (the per-rank work of a
+// DM-sharded step that does not shrink with the world size).
+template <typename InT>
+__global__ __launch_bounds__(256) void k_fx_patterns_x(const InT* __restrict__ x, InLayout lay,
+                                                       int64_t N, int64_t base, int64_t Qs,
+                                                       int64_t nR, int pad_mode,
+                                                       const float* __restrict__ padvals,
+                                                       const int4* __restrict__ pat,
+                                                       const int* __restrict__ gtab, int NG, int fx,
+                                                       uint4* __restrict__ P) {
+  extern __shared__ __attribute__((aligned(16))) uint4 L[];
+  const int g = blockIdx.x;
+  const int64_t j0 = (int64_t)blockIdx.y * kFxE;
+  const int p0 = gtab[g], p1 = gtab[g + 1];
+  const int lo = gtab[NG + 1 + 2 * g], hi = gtab[NG + 2 + 2 * g];
+  const int W = kFxE + hi - lo;
+  for (int k = 0; k < fx; ++k) {
+    const int c = g * fx + k;
+    const uint32_t pv = (pad_mode == PDD_PAD_VALUE) ? (uint32_t)padvals[c] : 0u;
+    for (int e = threadIdx.x; e < W; e += 256) {
+      const int64_t i = j0 + lo + e;
+      uint32_t v[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int64_t sm = base + i + m * Qs;
+        if (i < 0 || i >= nR) v[m] = 0u;
+        else if (sm >= 0 && sm < N) v[m] = x[lay.at(c, sm)];
+        else if (pad_mode == PDD_PAD_ROTATE) v[m] = x[lay.at(c, wrap_mod(sm, N))];
+        else v[m] = pv;
+      }
+      L[k * W + e] = make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16),
+                                v[6] | (v[7] << 16));
+    }
+  }
+  __syncthreads();
+  for (int p = p0; p < p1; ++p) {
+    const int4 q = pat[p];
+#pragma unroll
+    for (int e = threadIdx.x; e < kFxE; e += 256) {
+      const int64_t j = j0 + e;
+      if (j >= nR) break;
+      const uint4 a = L[e - lo], b = L[W + e - lo + q.y];
+      const uint4 c = fx > 2 ? L[2 * W + e - lo + q.z] : make_uint4(0u, 0u, 0u, 0u);
+      const uint4 d = fx > 3 ? L[3 * W + e - lo + q.w] : make_uint4(0u, 0u, 0u, 0u);
+      P[(int64_t)p * nR + j] = make_uint4(a.x + b.x + c.x + d.x, a.y + b.y + c.y + d.y,
+                                          a.z + b.z + c.z + d.z, a.w + b.w + c.w + d.w);
+    }
+  }
+}
+
 // n DMAs of 64 elements (1 KiB) each, q = first, first + step, ...
 __device__ __forceinline__ int stage_il_dma(uint32_t lds_dst, const float4* src, int ne, int first,
                                             int step, int lane) {
@@ -1564,8 +1619,11 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
                 "pdd_subband_chain: stage-2 image does not cover this plan");
   float4* R = nullptr;
   hipStream_t st = as_stream(stream);
+  // factorised plans with the LDS stage 1 build their pattern image straight
+  // from x (k_fx_patterns_x): no u16-eighths image R
+  const bool fx_direct = p->fx && p->d_gtab && !ex.R_pre && ds == 1;
   // C rows of the image + one row of zeros (the u16 kernel's pad channel)
-  if (!ex.R_pre) {
+  if (!ex.R_pre && !fx_direct) {
     R = static_cast<float4*>(scratch(st, kScratchImage, (size_t)((C + 1) * nr_alloc) * sizeof(float4)));
     if (!R) return -2;
   }
@@ -1585,8 +1643,8 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
     const int64_t nR = ex.R_pre ? ex.nR_pre : Qs + (hi - lo) + 64;
     if (ex.r2_pad && ex.r2_nR != 2 * Qs + ex.r2_ov) { rc = -4; break; }
     dim3 g1((unsigned)cdiv(nR, 256 * kIlPer), (unsigned)C);
-    if (ex.R_pre) {
-      // image built by the previous sweep
+    if (ex.R_pre || fx_direct) {
+      // image built by the previous sweep / none (factorised stage 1 reads x)
     } else if (hipMemsetAsync(R + C * nR, 0, (size_t)nR * sizeof(float4), st) != hipSuccess) {
       rc = -3;
       break;
@@ -1633,10 +1691,20 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
         rc = -3;
         break;
       }
-      if (p->d_gtab) {
-        const int NG = (int)(p->C / p->fx);
-        hipLaunchKernelGGL(k_fx_patterns_lds, dim3((unsigned)NG, (unsigned)cdiv(nR, kFxE)), dim3(256),
-                           (size_t)(p->fx * (kFxE + p->fx_rspan)) * sizeof(uint4), st, (const uint4*)R, nR,
+      const int NG = (int)(p->C / p->fx);
+      const dim3 gp((unsigned)NG, (unsigned)cdiv(nR, kFxE));
+      const size_t lds_p = (size_t)(p->fx * (kFxE + p->fx_rspan)) * sizeof(uint4);
+      const int64_t b0 = t_base + lo + x_off;
+      if (fx_direct && p->dtype == PDD_U8) {
+        hipLaunchKernelGGL(k_fx_patterns_x<uint8_t>, gp, dim3(256), lds_p, st, (const uint8_t*)x, lay,
+                           N, b0, Qs, nR, pad_mode, padvals, (const int4*)p->d_pat, p->d_gtab, NG,
+                           p->fx, P);
+      } else if (fx_direct) {
+        hipLaunchKernelGGL(k_fx_patterns_x<uint16_t>, gp, dim3(256), lds_p, st, (const uint16_t*)x,
+                           lay, N, b0, Qs, nR, pad_mode, padvals, (const int4*)p->d_pat, p->d_gtab,
+                           NG, p->fx, P);
+      } else if (p->d_gtab) {
+        hipLaunchKernelGGL(k_fx_patterns_lds, gp, dim3(256), lds_p, st, (const uint4*)R, nR,
                            (const int4*)p->d_pat, p->d_gtab, NG, p->fx, P);
       } else {
         hipLaunchKernelGGL(k_fx_patterns, dim3((unsigned)p->n_pat, (unsigned)cdiv(nR, 256 * kIlPer)),
@@ -2118,10 +2186,11 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
         if (e == hipSuccess && !T.gtab.empty()) e = hipMalloc(&p->d_gtab, T.gtab.size() * sizeof(int));
         if (e == hipSuccess && !T.gtab.empty())
           e = hipMemcpy(p->d_gtab, T.gtab.data(), T.gtab.size() * sizeof(int), hipMemcpyHostToDevice);
-        if (e == hipSuccess && !T.gtab.empty())
-          e = hipFuncSetAttribute((const void*)k_fx_patterns_lds,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)(4 * (kFxE + kFxRspan) * sizeof(uint4)));
+        for (const void* kf : {(const void*)k_fx_patterns_lds, (const void*)k_fx_patterns_x<uint8_t>,
+                               (const void*)k_fx_patterns_x<uint16_t>})
+          if (e == hipSuccess && !T.gtab.empty())
+            e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)(4 * (kFxE + kFxRspan) * sizeof(uint4)));
         if (e != hipSuccess) {
           set_error("pdd_sweep_plan_create: %s", hipGetErrorString(e));
           pdd_sweep_plan_destroy(p);
