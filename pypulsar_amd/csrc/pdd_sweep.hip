@@ -805,17 +805,24 @@ __device__ __forceinline__ int stage_il_dma(uint32_t lds_dst, const float4* src,
 // share one M0 value, the instruction offset (0 / 1024 / 2048 / 3072 bytes)
 // moving both the global source and the LDS destination
 // (scripts/probes/dma_offset.hip checks the LDS side on the device).
+#ifndef PDD_DMA_MODES
+#define PDD_DMA_MODES 0  // dev builds: PDD_SWEEP_DEBUG 512 / 1024 (timing only)
+#endif
 __device__ __forceinline__ int stage_il_dma_win(uint32_t lds_dst, const float4* src, int ne,
-                                                int lane) {
+                                                int lane, int nodma = 0) {
   const int nq = (ne + 63) >> 6;
-  for (int q = 0; q < nq; q += 4) {
-    const float4* s = src + q * 64 + lane;
-    const uint32_t m = __builtin_amdgcn_readfirstlane(lds_dst + q * 1024);
-    uint32_t keep;
-    switch (min(4, nq - q)) {
+  uint32_t keep;
 #define PDD_DMA_RUN(TEXT)                                                                      \
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t" TEXT "s_mov_b32 m0, %0" \
                : "=&s"(keep) : "v"(s), "s"(m) : "memory")
+  for (int q = 0; q < nq; q += 4) {
+    const float4* s = src + q * 64 + lane;
+    const uint32_t m = __builtin_amdgcn_readfirstlane(lds_dst + q * 1024);
+    if (PDD_DMA_MODES && (nodma & 512)) {  // timing only: everything but the DMAs
+      PDD_DMA_RUN("");
+      continue;
+    }
+    switch ((PDD_DMA_MODES && (nodma & 1024)) ? 1 : min(4, nq - q)) {  // (1024, timing only: a run's first DMA)
       case 1: PDD_DMA_RUN("global_load_lds_dwordx4 %1, off\n\t"); break;
       case 2: PDD_DMA_RUN("global_load_lds_dwordx4 %1, off\n\t"
                           "global_load_lds_dwordx4 %1, off offset:1024\n\t"); break;
@@ -834,6 +841,39 @@ __device__ __forceinline__ int stage_il_dma_win(uint32_t lds_dst, const float4* 
 #ifndef PDD_IL_DMA_WIN
 #define PDD_IL_DMA_WIN 1
 #endif
+
+// The same from a wave-uniform source address in an SGPR pair (the saddr
+// form; the lanes' VGPR offset is lane * 16 for every DMA): the DMAs take no
+// VALU address arithmetic.  `nq` pieces of 64 elements.
+__device__ __forceinline__ int stage_il_dma_s(uint32_t lds_dst, const float4* src, int nq,
+                                              uint32_t voff, int mode = 0) {
+  for (int q = 0; q < nq; q += 4) {
+    const float4* s = src + q * 64;
+    const uint32_t m = lds_dst + q * 1024;
+    uint32_t keep;
+#define PDD_DMA_S(TEXT)                                                                        \
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t" TEXT "s_mov_b32 m0, %0" \
+               : "=&s"(keep) : "v"(voff), "s"(s), "s"(m) : "memory")
+    if (PDD_DMA_MODES && (mode & 512)) {  // timing only: everything but the DMAs
+      PDD_DMA_S("");
+      continue;
+    }
+    switch ((PDD_DMA_MODES && (mode & 1024)) ? 1 : min(4, nq - q)) {  // (1024, timing only: a run's first DMA)
+      case 1: PDD_DMA_S("global_load_lds_dwordx4 %1, %2\n\t"); break;
+      case 2: PDD_DMA_S("global_load_lds_dwordx4 %1, %2\n\t"
+                        "global_load_lds_dwordx4 %1, %2 offset:1024\n\t"); break;
+      case 3: PDD_DMA_S("global_load_lds_dwordx4 %1, %2\n\t"
+                        "global_load_lds_dwordx4 %1, %2 offset:1024\n\t"
+                        "global_load_lds_dwordx4 %1, %2 offset:2048\n\t"); break;
+      default: PDD_DMA_S("global_load_lds_dwordx4 %1, %2\n\t"
+                         "global_load_lds_dwordx4 %1, %2 offset:1024\n\t"
+                         "global_load_lds_dwordx4 %1, %2 offset:2048\n\t"
+                         "global_load_lds_dwordx4 %1, %2 offset:3072\n\t"); break;
+#undef PDD_DMA_S
+    }
+  }
+  return nq;
+}
 
 // Synchronisation of k_sweep_il: one s_barrier per chunk.  Before barrier k
 // the loader waves retire chunk k's DMAs with a counted vmcnt (chunks k+1 ..
@@ -954,7 +994,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const int* __restrict__ cht, int maxch, float* __restrict__ out, int64_t ld_out, int D,
     int64_t Qs, int64_t t_base, int64_t n_out, int buf_e, int n_tblk, int n_dblk, int dbg,
     int64_t row_g, int64_t row_d, int flush_n, float out_bias, const float* __restrict__ r2_pad,
-    int64_t r2_nR, int64_t r2_ov, const int4* __restrict__ wt) {
+    int64_t r2_nR, int64_t r2_ov, const int4* __restrict__ wt, int fx_stage) {
   // Grouped sweeps: C is the channel count of ONE group; blockIdx.x / (tiles
   // per group) is the group, whose channels are R rows [grp*C, grp*C + C),
   // whose tables are mt[grp][...], and whose trial d lands in plane row
@@ -986,6 +1026,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   int dblk, tblk;                                                             \
   const int grp = tile / per_grp;                                             \
   il_tile_of(tile - grp * per_grp, n_tblk, n_dblk, dbg, dblk, tblk);          \
+  if (PDD_DMA_MODES && (dbg & 384)) tblk = (dbg & 128) ? 0 : (tblk & 7);          \
   const float4* R = R0 + (int64_t)grp * C * nR;                               \
   const int64_t t0 = (int64_t)tblk * Tq;                                      \
   const int* mt_b = mt + ((int64_t)grp * n_dblk + dblk) * (C + 1) * ROW;      \
@@ -1001,6 +1042,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   // configs[3] 101.6 -> 116.4 ms per launch: the staging does not scale
   // with the issuing waves.)
   const uint32_t img_lds = lds_addr_of(img);
+  const uint32_t voff16 = (uint32_t)lane * 16u;
   const int4* wt_b = FX ? wt + ((int64_t)grp * n_dblk + dblk) * maxch * kFxWin : nullptr;
   auto fx_rec = [&](int k) -> int4 {
     if constexpr (FX) return wt_b[(int64_t)min(k, nchunk - 1) * kFxWin + lane];
@@ -1013,6 +1055,21 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const int b = k % NBUF;
     const int nw = __builtin_amdgcn_readlane(rec.w, 0) >> 20;
     int n = 0;
+    if (fx_stage) {
+      // lane i = window i: its source, LDS address and piece count in one
+      // pass, then this loader's windows (i = first mod step) from SGPRs
+      const uint64_t sv = (uint64_t)(R + (int64_t)(rec.w & 0xfffff) * nR + (t0 + rec.x - lo));
+      const uint32_t dv = img_lds + (uint32_t)((b * buf_e + rec.z) * 16);
+      const int qv = (rec.y + 63) >> 6;
+      for (int i = first; i < nw; i += step) {
+        const uint32_t lo32 = __builtin_amdgcn_readlane((uint32_t)sv, i);
+        const uint32_t hi32 = __builtin_amdgcn_readlane((uint32_t)(sv >> 32), i);
+        n += stage_il_dma_s(__builtin_amdgcn_readlane(dv, i),
+                            (const float4*)(((uint64_t)hi32 << 32) | lo32),
+                            __builtin_amdgcn_readlane(qv, i), voff16, dbg & 1536);
+      }
+      return n;
+    }
     for (int i = 0; i < nw; ++i) {
       const int bm = __builtin_amdgcn_readlane(rec.x, i);
       const int len = __builtin_amdgcn_readlane(rec.y, i);
@@ -1022,7 +1079,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
         // window i from loader i mod NLW, its DMAs in runs sharing M0
         if (i % step == first)
           n += stage_il_dma_win(img_lds + (uint32_t)((b * buf_e + off) * 16),
-                                R + (int64_t)row * nR + (t0 + bm - lo), len, lane);
+                                R + (int64_t)row * nR + (t0 + bm - lo), len, lane, dbg & 1536);
       } else {
         n += stage_il_dma(img_lds + (uint32_t)((b * buf_e + off) * 16),
                           R + (int64_t)row * nR + (t0 + bm - lo), len, first, step, lane);
@@ -1435,7 +1492,7 @@ static constexpr int kLdsMax = 160 * 1024;
 
 typedef void (*sweep_il_fn)(const float4*, int64_t, int, int, const int*, const int*, int, float*,
                             int64_t, int, int64_t, int64_t, int64_t, int, int, int, int, int64_t,
-                            int64_t, int, float, const float*, int64_t, int64_t, const int4*);
+                            int64_t, int, float, const float*, int64_t, int64_t, const int4*, int);
 static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false) {
   if (fx) {
     if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
@@ -1500,6 +1557,16 @@ static int debug_flags() {
   return 0;
 #endif
 }
+// Factorised staging: the loaders' per-window work from SGPRs (lane i
+// computes window i's addresses once per chunk; each loader walks only its
+// own windows) for groups of 4, whose stage 2 is loader-bound; groups of 2
+// keep the per-lane address form (profiles/r3_staging_probe.txt section 8).
+static int fx_stage_for(int g) {
+#ifdef PDD_SWEEP_DEV
+  if (const char* e = getenv("PDD_FX_STAGE")) return atoi(e);
+#endif
+  return g == 4 ? 1 : 0;
+}
 static int forced_variant() {
 #ifdef PDD_SWEEP_DEV
   const char* e = getenv("PDD_SWEEP_VARIANT");
@@ -1528,6 +1595,7 @@ struct pdd_sweep_plan {
   uint8_t* d_rows = nullptr;
   int rows_max = 0, nchunk = 0;
   int fx = 0;              // factorised sweep: channels per group (0 = channel by channel)
+  int fx_stage = 0;        // factorised: loaders stage from SGPR window addresses (k_sweep_il)
   int64_t n_pat = 0;       // factorised: pattern series (stage-1 rows, + 1 zero row)
   int64_t fx_rows = 0;     // factorised: metadata rows per trial block (groups + pad groups)
   int fx_rspan = 0;        // factorised: widest relative-shift range of a group (stage-1 LDS)
@@ -1724,7 +1792,7 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
                        (int)(p->fx ? p->fx_rows - 1 : p->C), (int)lo, p->d_tab,
                        p->d_bmin, p->maxch, out, ld_out, (int)p->D, Qs, t_base, t_base + cnt,
                        p->stride, (int)n_tblk, (int)p->n_dblk, dbg, row_g, row_d, flush_n, out_bias,
-                       ex.r2_pad, ex.r2_nR, ex.r2_ov, (const int4*)p->d_wt);
+                       ex.r2_pad, ex.r2_nR, ex.r2_ov, (const int4*)p->d_wt, p->fx_stage);
     if (hipGetLastError() != hipSuccess) rc = -3;
     if (bracket) {
       (void)hipEventRecord(p->ev[2 * p->timed + 1], st);
@@ -1951,8 +2019,9 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
     for (size_t k = 0; k < l.size(); ++k) {
       T.cht[(size_t)(b * (maxch + 1) + 1 + k)] = l[k];
       const auto& r = cw[(size_t)b][k];
+      int* o = &T.wt[((size_t)b * maxch + k) * kFxWin * 4];
       for (size_t i = 0; i < r.size(); ++i)
-        for (int f = 0; f < 4; ++f) T.wt[(((size_t)b * maxch + k) * kFxWin + i) * 4 + f] = r[i][f];
+        for (int f = 0; f < 4; ++f) o[i * 4 + f] = r[i][f];
     }
   }
   return true;
@@ -2171,6 +2240,7 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
       }
       if (fxg) {
         p->fx = fxg;
+        p->fx_stage = fx_stage_for(fxg);
         p->n_pat = T.n_pat;
         p->fx_rows = T.rows_pb;
         p->fx_rspan = T.rspan;  // stage 1 sizes its LDS to it: more workgroups per CU

@@ -8,7 +8,7 @@ mkdir -p gpurun_out/ab
 for cfg in ${CFGS:-"config3:u8" "config2:u8" "config2:f32"}; do
   c=${cfg%%:*}; dt=${cfg##*:}
   for lib in ${LIBS:-base dev}; do
-    PDD_DEV_LIB=build/libpdd_$lib.so timeout -k 10 200 python bench.py --config $c --dtype $dt --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-e2e > gpurun_out/ab/b.json 2> gpurun_out/ab/b.err || { echo "FAIL $c $dt $lib"; tail -3 gpurun_out/ab/b.err; exit 1; }
+    PDD_DEV_LIB=build/libpdd_$lib.so timeout -k 10 200 python bench.py --config $c --dtype $dt --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-e2e ${BARGS} > gpurun_out/ab/b.json 2> gpurun_out/ab/b.err || { echo "FAIL $c $dt $lib"; tail -3 gpurun_out/ab/b.err; exit 1; }
     python -c "
 import json;d=json.load(open('gpurun_out/ab/b.json'));r=d['roofline'];p=d['config']['plan']
 print('$c $dt %-6s variant %s kernel %.2f ms  %.2f T  step %.1f ms' % ('$lib', p['variant'], r['kernel_ms_per_launch'], r['achieved'], d['ms_per_step']))"
