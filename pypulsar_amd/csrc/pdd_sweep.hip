@@ -849,7 +849,7 @@ __device__ __forceinline__ int stage_il_dma_s(uint32_t lds_dst, const float4* sr
                                               uint32_t voff, int mode = 0) {
   for (int q = 0; q < nq; q += 4) {
     const float4* s = src + q * 64;
-    const uint32_t m = lds_dst + q * 1024;
+    const uint32_t m = __builtin_amdgcn_readfirstlane(lds_dst + q * 1024);
     uint32_t keep;
 #define PDD_DMA_S(TEXT)                                                                        \
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t" TEXT "s_mov_b32 m0, %0" \
@@ -1055,6 +1055,20 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const int b = k % NBUF;
     const int nw = __builtin_amdgcn_readlane(rec.w, 0) >> 20;
     int n = 0;
+    if (FX && fx_stage == 2) {
+      // this loader's windows by scalar loads (lgkmcnt: no wait on the DMAs)
+      const int4* lst = wt_b + (int64_t)k * kFxWin + first * 16;
+      int4 r = lst[0];
+      const int nown = r.w >> 16;
+      for (int j = 0; j < nown; ++j) {
+        const int4 nx = lst[min(j + 1, 15)];
+        n += stage_il_dma_s(img_lds + (uint32_t)((b * buf_e + r.z) * 16),
+                            R + ((int64_t)r.x * nR + (t0 + r.y - lo)), r.w & 0xffff, voff16,
+                            dbg & 1536);
+        r = nx;
+      }
+      return n;
+    }
     if (fx_stage) {
       // lane i = window i: its source, LDS address and piece count in one
       // pass, then this loader's windows (i = first mod step) from SGPRs
@@ -1114,10 +1128,11 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       }
       return n;
     };
-    int4 rec_next = fx_rec(0);
+    int4 rec_next = fx_stage == 2 ? make_int4(0, 0, 0, 0) : fx_rec(0);
     auto issue_samples = [&](int k) -> int {
       if (dbg & 1) return 0;
       if constexpr (FX) {
+        if (fx_stage == 2) return fx_issue(k, rec_next, lw, NLW);  // scalar-loaded records
         // the record of chunk k was loaded an iteration ahead (the wait for
         // it is the one this iteration already did); load chunk k + 1's now
         const int4 rec = rec_next;
@@ -2241,6 +2256,26 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
       if (fxg) {
         p->fx = fxg;
         p->fx_stage = fx_stage_for(fxg);
+        if (p->fx_stage == 2) {
+          // per loader lists (window i -> loader i mod 4, slot i / 4):
+          // {row, bmin, buffer offset, pieces | own windows << 16}
+          std::vector<int> w2(T.wt.size(), 0);
+          const size_t nchk = T.wt.size() / (kFxWin * 4);
+          for (size_t c = 0; c < nchk; ++c) {
+            const int* src = &T.wt[c * kFxWin * 4];
+            int* dst = &w2[c * kFxWin * 4];
+            const int nw = src[3] >> 20;
+            for (int i = 0; i < nw; ++i) {
+              int* q = dst + ((i % 4) * 16 + i / 4) * 4;
+              q[0] = src[i * 4 + 3] & 0xfffff;
+              q[1] = src[i * 4];
+              q[2] = src[i * 4 + 2];
+              q[3] = (src[i * 4 + 1] + 63) / 64;
+            }
+            for (int l = 0; l < 4; ++l) dst[l * 64 + 3] |= ((nw - l + 3) / 4) << 16;
+          }
+          T.wt.swap(w2);
+        }
         p->n_pat = T.n_pat;
         p->fx_rows = T.rows_pb;
         p->fx_rspan = T.rspan;  // stage 1 sizes its LDS to it: more workgroups per CU
