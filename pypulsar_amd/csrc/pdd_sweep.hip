@@ -988,13 +988,14 @@ __device__ __forceinline__ uint32_t add3_u32(uint32_t a, uint32_t b, uint32_t c)
 // pattern row | window count << 20}, read by one vector load per loader lane
 // an iteration ahead.
 constexpr int kFxWin = 64;
-template <int G, int DPW, int NCW, int NLW, int CC, int NBUF, bool U16 = false, bool FX = false>
+template <int G, int DPW, int NCW, int NLW, int CC, int NBUF, bool U16 = false, bool FX = false,
+          int FXS = 0>
 __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const float4* __restrict__ R0, int64_t nR, int C, int lo, const int* __restrict__ mt,
     const int* __restrict__ cht, int maxch, float* __restrict__ out, int64_t ld_out, int D,
     int64_t Qs, int64_t t_base, int64_t n_out, int buf_e, int n_tblk, int n_dblk, int dbg,
     int64_t row_g, int64_t row_d, int flush_n, float out_bias, const float* __restrict__ r2_pad,
-    int64_t r2_nR, int64_t r2_ov, const int4* __restrict__ wt, int fx_stage) {
+    int64_t r2_nR, int64_t r2_ov, const int4* __restrict__ wt) {
   // Grouped sweeps: C is the channel count of ONE group; blockIdx.x / (tiles
   // per group) is the group, whose channels are R rows [grp*C, grp*C + C),
   // whose tables are mt[grp][...], and whose trial d lands in plane row
@@ -1055,21 +1056,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const int b = k % NBUF;
     const int nw = __builtin_amdgcn_readlane(rec.w, 0) >> 20;
     int n = 0;
-    if (FX && fx_stage == 2) {
-      // this loader's windows by scalar loads (lgkmcnt: no wait on the DMAs)
-      const int4* lst = wt_b + (int64_t)k * kFxWin + first * 16;
-      int4 r = lst[0];
-      const int nown = r.w >> 16;
-      for (int j = 0; j < nown; ++j) {
-        const int4 nx = lst[min(j + 1, 15)];
-        n += stage_il_dma_s(img_lds + (uint32_t)((b * buf_e + r.z) * 16),
-                            R + ((int64_t)r.x * nR + (t0 + r.y - lo)), r.w & 0xffff, voff16,
-                            dbg & 1536);
-        r = nx;
-      }
-      return n;
-    }
-    if (fx_stage) {
+    if constexpr (FXS == 1) {
       // lane i = window i: its source, LDS address and piece count in one
       // pass, then this loader's windows (i = first mod step) from SGPRs
       const uint64_t sv = (uint64_t)(R + (int64_t)(rec.w & 0xfffff) * nR + (t0 + rec.x - lo));
@@ -1128,11 +1115,10 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       }
       return n;
     };
-    int4 rec_next = fx_stage == 2 ? make_int4(0, 0, 0, 0) : fx_rec(0);
+    int4 rec_next = fx_rec(0);
     auto issue_samples = [&](int k) -> int {
       if (dbg & 1) return 0;
       if constexpr (FX) {
-        if (fx_stage == 2) return fx_issue(k, rec_next, lw, NLW);  // scalar-loaded records
         // the record of chunk k was loaded an iteration ahead (the wait for
         // it is the one this iteration already did); load chunk k + 1's now
         const int4 rec = rec_next;
@@ -1507,11 +1493,14 @@ static constexpr int kLdsMax = 160 * 1024;
 
 typedef void (*sweep_il_fn)(const float4*, int64_t, int, int, const int*, const int*, int, float*,
                             int64_t, int, int64_t, int64_t, int64_t, int, int, int, int, int64_t,
-                            int64_t, int, float, const float*, int64_t, int64_t, const int4*, int);
-static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false) {
+                            int64_t, int, float, const float*, int64_t, int64_t, const int4*);
+static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false, int fxs = 0) {
   if (fx) {
+    // (the staging form is a template parameter: a runtime switch between
+    // the two cost the north star's per-lane form 25%)
     if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
-      return k_sweep_il<2, 4, 12, 4, 8, 2, true, true>;
+      return fxs == 1 ? k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 1>
+                      : k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 0>;
     return nullptr;
   }
 #define IL(NCW_, NLW_, CC_, NB_)                                                              \
@@ -1802,12 +1791,12 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
     const bool bracket = p->timing && p->timed < pdd_sweep_plan::kEvPairs;
     if (p->timing && !bracket) pm->dropped++;
     if (bracket) (void)hipEventRecord(p->ev[2 * p->timed], st);
-    hipLaunchKernelGGL(il_kernel_for(p->v, p->fx != 0), dim3((unsigned)blocks), dim3(p->v.threads()),
+    hipLaunchKernelGGL(il_kernel_for(p->v, p->fx != 0, p->fx_stage), dim3((unsigned)blocks), dim3(p->v.threads()),
                        p->lds_bytes, st, ex.R_pre ? ex.R_pre : (p->fx ? (const float4*)P : R), nR,
                        (int)(p->fx ? p->fx_rows - 1 : p->C), (int)lo, p->d_tab,
                        p->d_bmin, p->maxch, out, ld_out, (int)p->D, Qs, t_base, t_base + cnt,
                        p->stride, (int)n_tblk, (int)p->n_dblk, dbg, row_g, row_d, flush_n, out_bias,
-                       ex.r2_pad, ex.r2_nR, ex.r2_ov, (const int4*)p->d_wt, p->fx_stage);
+                       ex.r2_pad, ex.r2_nR, ex.r2_ov, (const int4*)p->d_wt);
     if (hipGetLastError() != hipSuccess) rc = -3;
     if (bracket) {
       (void)hipEventRecord(p->ev[2 * p->timed + 1], st);
@@ -2256,26 +2245,6 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
       if (fxg) {
         p->fx = fxg;
         p->fx_stage = fx_stage_for(fxg);
-        if (p->fx_stage == 2) {
-          // per loader lists (window i -> loader i mod 4, slot i / 4):
-          // {row, bmin, buffer offset, pieces | own windows << 16}
-          std::vector<int> w2(T.wt.size(), 0);
-          const size_t nchk = T.wt.size() / (kFxWin * 4);
-          for (size_t c = 0; c < nchk; ++c) {
-            const int* src = &T.wt[c * kFxWin * 4];
-            int* dst = &w2[c * kFxWin * 4];
-            const int nw = src[3] >> 20;
-            for (int i = 0; i < nw; ++i) {
-              int* q = dst + ((i % 4) * 16 + i / 4) * 4;
-              q[0] = src[i * 4 + 3] & 0xfffff;
-              q[1] = src[i * 4];
-              q[2] = src[i * 4 + 2];
-              q[3] = (src[i * 4 + 1] + 63) / 64;
-            }
-            for (int l = 0; l < 4; ++l) dst[l * 64 + 3] |= ((nw - l + 3) / 4) << 16;
-          }
-          T.wt.swap(w2);
-        }
         p->n_pat = T.n_pat;
         p->fx_rows = T.rows_pb;
         p->fx_rspan = T.rspan;  // stage 1 sizes its LDS to it: more workgroups per CU
@@ -2317,7 +2286,7 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
       return -2;
     }
     if (p->lds_bytes > 64 * 1024) {
-      const void* kf = il ? (const void*)il_kernel_for(v, p->fx != 0) : (const void*)kernel_for(v);
+      const void* kf = il ? (const void*)il_kernel_for(v, p->fx != 0, p->fx_stage) : (const void*)kernel_for(v);
       e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, p->lds_bytes);
       if (e != hipSuccess) {
         set_error("pdd_sweep_plan_create: hipFuncSetAttribute: %s", hipGetErrorString(e));
