@@ -46,6 +46,22 @@ EXPORTS = (
 )
 
 
+def source_digest():
+    """sha256 (first 16 hex digits) of the HIP sources libpdd.so is built
+    from.  Profiling evidence (profiles/pmc_sweep.json) is stamped with it, so
+    bench.py can refuse counters measured on a different build."""
+    import hashlib
+    csrc = os.path.join(_HERE, "csrc")
+    h = hashlib.sha256()
+    names = sorted(n for n in os.listdir(csrc) if n.endswith((".hip", ".h")))
+    for n in names:
+        with open(os.path.join(csrc, n), "rb") as f:
+            h.update(n.encode() + b"\0" + f.read())
+    with open(os.path.join(os.path.dirname(_HERE), "include", "pdd.h"), "rb") as f:
+        h.update(b"pdd.h\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 class PddLibraryMissing(RuntimeError):
     pass
 

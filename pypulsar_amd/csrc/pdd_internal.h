@@ -54,6 +54,9 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // message on failure.
 enum { kScratchImage = 0, kScratchChain = 1, kScratchPartial = 2, kScratchSmall = 3, kScratchPattern = 4 };
 void* scratch(hipStream_t st, int slot, size_t bytes);
+// Bytes the calling thread's (stream, slot) buffer holds now (0: none): memory
+// a larger request of the same slot would free before allocating.
+size_t scratch_held(hipStream_t st, int slot);
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

@@ -76,6 +76,16 @@ void* scratch(hipStream_t st, int slot, size_t bytes) {
   return p;
 }
 
+size_t scratch_held(hipStream_t st, int slot) {
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  const std::thread::id tid = std::this_thread::get_id();
+  for (const auto& b : g_scratch)
+    if (b.dev == dev && b.st == st && b.tid == tid && b.slot == slot) return b.bytes;
+  return 0;
+}
+
 // ---------------------------------------------------------------- loaders
 template <typename T>
 __device__ __forceinline__ float to_f32(T v) { return static_cast<float>(v); }

@@ -1634,8 +1634,11 @@ using namespace pdd;
 // sweep was built by the previous one (quarter length Qs_pre, nR_pre
 // elements per row): no interleave pre-pass, one segment.
 // Output samples one segment of the interleaved path can hold (<= 0: the
-// delay span alone exceeds the scratch budget of R).
-static int64_t il_seg_samples(const pdd_sweep_plan* p) {
+// delay span alone exceeds the scratch budget of R).  The budget is capped
+// by the device memory free now (plus what this stream's image / pattern
+// slots already hold): a smaller GPU or a busier one gets more, shorter
+// segments instead of a scratch allocation failure.
+static int64_t il_seg_samples(const pdd_sweep_plan* p, hipStream_t st) {
   const int Tq = 64 * p->v.G;
   const int64_t C = p->C * p->n_grp;
   const int64_t lo = std::min(0, p->min_bin), hi = std::max(0, p->max_bin);
@@ -1645,7 +1648,18 @@ static int64_t il_seg_samples(const pdd_sweep_plan* p) {
   // factorised plans also hold the stage-1 pattern image (n_pat + 1 rows)
   const int64_t rows = C + (p->fx ? p->n_pat + 2 : 0);
   if (p->fx) budget = (int64_t)40 << 30;
-  if (const char* e = getenv("PDD_SWEEP_SEG_BYTES")) budget = std::max<int64_t>(atoll(e), 1 << 16);
+  if (const char* e = getenv("PDD_SWEEP_SEG_BYTES")) {
+    budget = std::max<int64_t>(atoll(e), 1 << 16);
+  } else {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+      const int64_t avail = (int64_t)fr + (int64_t)scratch_held(st, kScratchImage) +
+                            (p->fx ? (int64_t)scratch_held(st, kScratchPattern) : 0);
+      // keep 1/8 of it and 512 MiB for the caller
+      budget = std::min(budget, std::max<int64_t>(avail - avail / 8 - ((int64_t)512 << 20),
+                                                  (int64_t)64 << 20));
+    }
+  }
   const int64_t nr_max = budget / (rows * 16);
   return (nr_max - (hi - lo) - 64) / Tq * Tq * p->v.S;
 }
@@ -1674,7 +1688,7 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
   const int flush_n = std::min(256, 65535 / (vmax * std::max(1, p->fx)));
   const int64_t C = p->C * p->n_grp;  // all channels (groups are contiguous channel ranges)
   const int64_t lo = std::min(0, p->min_bin), hi = std::max(0, p->max_bin);
-  int64_t seg = il_seg_samples(p);  // output samples per segment
+  int64_t seg = il_seg_samples(p, as_stream(stream));  // output samples per segment
   PDD_REQUIRE(seg > 0, "pdd_sweep_execute: delay span %lld too wide for the segment budget",
               (long long)(hi - lo));
   // equal segments (whole tiles): every launch does the same work
@@ -1702,8 +1716,10 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
   // factorised plans: the pattern image (stage 1), n_pat rows + a row of zeros
   uint4* P = nullptr;
   if (p->fx) {
-    PDD_REQUIRE(u16 && p->dtype != PDD_F32 && ds == 1 && !ex.r2_pad && !ex.R_pre && p->n_grp == 1,
-                "pdd_sweep_execute: factorised plans take 8/16-bit input at the raw rate");
+    // (ds > 1: the interleave pre-pass co-adds the raw rows into R and stage
+    // 1 builds the patterns from R: sums of fx co-adds <= 4 * 1020 stay exact)
+    PDD_REQUIRE(u16 && p->dtype != PDD_F32 && !ex.r2_pad && !ex.R_pre && p->n_grp == 1,
+                "pdd_sweep_execute: factorised plans take single-group 8/16-bit input");
     P = static_cast<uint4*>(scratch(st, kScratchPattern, (size_t)((p->n_pat + 1) * nr_alloc) * sizeof(uint4)));
     if (!P) return -2;
   }
@@ -2432,8 +2448,8 @@ int pdd_subband_chain(const pdd_sweep_plan* p1, const void* x, int64_t n_raw, in
   // reads quarters of length 2 Qs1 (a multiple of its 256-element tile)
   const int64_t Qs1 = cdiv(cdiv(N1, 8), 64 * p1->v.G) * (64 * p1->v.G);
   const int64_t ov = std::max(0, p2->max_bin) + 64;
-  if (!(ov <= Qs1 && (2 * Qs1) % (64 * p2->v.G) == 0 && il_seg_samples(p1) >= N1 &&
-        il_seg_samples(p2) >= n_out)) {
+  if (!(ov <= Qs1 && (2 * Qs1) % (64 * p2->v.G) == 0 && il_seg_samples(p1, as_stream(stream)) >= N1 &&
+        il_seg_samples(p2, as_stream(stream)) >= n_out)) {
     set_error("pdd_subband_chain: block of %lld samples does not chain (stage-2 span %d, "
               "one segment per stage needed)", (long long)N1, p2->max_bin);
     return PDD_ENOCHAIN;  // nothing launched: run the stages apart

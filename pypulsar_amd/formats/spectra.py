@@ -152,6 +152,23 @@ class HostView(np.ndarray):
         super(HostView, self).__setitem__(key, value)
         self._push()
 
+    # in-place ndarray methods that bypass __setitem__ and ufuncs
+    def fill(self, value):
+        np.ndarray.fill(self, value)
+        self._push()
+
+    def put(self, *args, **kwargs):
+        np.ndarray.put(self, *args, **kwargs)
+        self._push()
+
+    def sort(self, *args, **kwargs):
+        np.ndarray.sort(self, *args, **kwargs)
+        self._push()
+
+    def partition(self, *args, **kwargs):
+        np.ndarray.partition(self, *args, **kwargs)
+        self._push()
+
     def __array_ufunc__(self, ufunc, method, *inputs, **kwargs):
         args = [np.asarray(a).view(np.ndarray) if isinstance(a, HostView) else a for a in inputs]
         outs = kwargs.get("out")
@@ -231,10 +248,13 @@ class Spectra(object):
 
     def _upload_host(self, arr):
         """Write a full [numchans, numspectra] host array back (HostView).
-        The device now equals the shared host copy, so the version (and the
-        copy's validity) is unchanged."""
+        The shared host copy is rounded in place to the float32 values the
+        device now holds, so it stays equal to the device and the version
+        (and the copy's validity) is unchanged."""
         assert arr.shape == tuple(self._x.shape)
-        self._x.copy_(torch.from_numpy(np.ascontiguousarray(arr, dtype=np.float32)))
+        f32 = np.ascontiguousarray(arr, dtype=np.float32)
+        self._x.copy_(torch.from_numpy(f32))
+        arr[...] = f32
         self._raw8 = None
 
     def _set(self, x):

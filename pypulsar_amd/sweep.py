@@ -190,14 +190,16 @@ class DMSweep(object):
         elif x.dtype in _U16_TYPES:
             code = _lib.U16
             mode, pv = _pads16(x, self.C, padval)
-            if self.input_max is not None and mode == _lib.PAD_VALUE and float(padval) > self.input_max:
-                raise ValueError("pad %g above the sweep's input bound %d" % (float(padval),
-                                                                             self.input_max))
         elif x.dtype == torch.float32:
             code = _lib.F32
             mode, pv = _pad_args(x, padval)
         else:
             raise TypeError("sweep input must be float32, uint8 or 16-bit")
+        if code != _lib.F32 and self.input_max is not None and mode == _lib.PAD_VALUE \
+                and float(padval) > self.input_max:
+            # the packed-u16 flush interval assumes every summed value <= input_max
+            raise ValueError("pad %g above the sweep's input bound %d" % (float(padval),
+                                                                         self.input_max))
         call("pdd_sweep_execute_ex", self._plan(code), ptr(x), N, x.stride(0), 0, 0, mode, ptr(pv),
              ptr(out), out.stride(0), n_out, float(out_bias), stream_ptr(stream))
         return out

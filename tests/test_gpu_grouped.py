@@ -172,6 +172,34 @@ def test_sweep_ds_fused_downsample(gpu, ds, padval, layout):
     gs.close()
 
 
+@pytest.mark.parametrize("ds", [2, 3, 4])
+@pytest.mark.parametrize("padval", [0, 17, "rotate"])
+@pytest.mark.parametrize("factor", ["force4", "force2", True])
+def test_sweep_ds_factorised(gpu, ds, padval, factor):
+    """sweep_ds (and so DDplanExecutor's one-stage steps at downsamp 2..4) on
+    a dtype='u16' plan that IS factorised: the interleave pre-pass co-adds
+    the raw rows, stage 1 builds the patterns from that image, and the plane
+    equals the oracle's Spectra.downsample + per-trial sweep bit for bit.
+    factor=True: whatever the planner picks for this grid."""
+    import torch
+    from pypulsar_amd import _lib
+    from pypulsar_amd.sweep import DMSweep
+    C, n_raw = 128, (1 << 14) + 5
+    x = u8_data(C, n_raw, 60 + ds)
+    x8 = torch.from_numpy(x).cuda()
+    dms = np.linspace(0.0, 12.0, 96)
+    sw = DMSweep(dms, band(C), DT * ds, dtype="u16", factor=factor)
+    g = sw.factor_info(_lib.U16)[0]
+    if factor is not True:
+        assert g == int(factor[-1]), g
+    N = n_raw // ds
+    got = sw.sweep_ds(x8, ds, padval=padval, n_out=N).cpu().numpy()
+    xd, _ = orc.downsample(x.astype(np.float64), DT, ds)
+    ref = orc.sweep_plane(xd, sw.table, padval=padval, n_out=N)
+    np.testing.assert_array_equal(got, ref)
+    sw.close()
+
+
 @pytest.mark.parametrize("ds", [1, 2, 4])
 @pytest.mark.parametrize("padval", [0, 9])
 def test_subband_chain_equals_stages(gpu, ds, padval):

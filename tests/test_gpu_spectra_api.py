@@ -87,3 +87,27 @@ def test_two_open_views_both_write_through(gpu):
     want[:, 5] = 1.0
     np.testing.assert_array_equal(s.get_chan(3), want[3])
     np.testing.assert_array_equal(s.data, want)
+
+
+@pytest.mark.gpu
+def test_inplace_methods_and_float32_rounding_write_through(gpu):
+    """in-place ndarray methods that skip __setitem__ / ufuncs
+    (fill, put, sort) write through, and a float64 value that rounds in the
+    float32 upload leaves the shared host copy equal to the device."""
+    import torch
+    from pypulsar_amd.formats.spectra import Spectra
+    C, N = 4, 256
+    x = u8_data(C, N, 11)
+    s = Spectra(band(C), DT, x)
+    s.get_chan(0).fill(2.0)
+    np.testing.assert_array_equal(s._x[0].cpu().numpy(), np.full(N, 2.0, np.float32))
+    s.get_chan(1).put([0, 3], [5.0, 6.0])
+    assert s._x[1, 0].item() == 5.0 and s._x[1, 3].item() == 6.0
+    c2 = s.get_chan(2)
+    c2.sort()
+    np.testing.assert_array_equal(s._x[2].cpu().numpy(), np.sort(x[2]).astype(np.float32))
+    v = 0.1  # not a float32 value
+    s.get_chan(3)[:] = v
+    host = s.data
+    assert host[3, 0] == np.float64(np.float32(v))
+    np.testing.assert_array_equal(host, s._x.to(torch.float64).cpu().numpy())
