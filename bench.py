@@ -230,13 +230,24 @@ def _cpu_pool(x, freqs, dt, dms, orc, workers=None, ntrials=None, cblk=64):
                        "C-order, %.1f s" % (ntrials, cblk, workers, el))
 
 
-def load_pmc(path, key):
+def load_pmc(path, key, plan=None):
+    """profiles/pmc_sweep.json[key] if it was measured on THIS build: the
+    entry's source digest (scripts/collect_profiles.py) must equal the
+    library sources' digest and its sweep plan the running plan; stale
+    counters are refused (None)."""
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d.get(key)
+            e = json.load(f).get(key)
     except Exception:
         return None
+    if not isinstance(e, dict):
+        return None
+    from pypulsar_amd._lib import source_digest
+    if e.get("src_digest") != source_digest():
+        return None
+    if plan is not None and e.get("plan") is not None and e.get("plan") != plan:
+        return None
+    return e
 
 
 def _free_port():
@@ -492,11 +503,13 @@ def sweep_bench(args, cfg, rank, world, dev):
         pmc_key = "config3_channel"
     elif args.config == "northstar":
         pmc_key = "northstar"
-    pmc = load_pmc(os.path.join(ROOT, "profiles", "pmc_sweep.json"), pmc_key)
-    traffic = pmc.get("hbm_bytes_per_launch") if isinstance(pmc, dict) else None
+    plan = sw.info(1 if dtype == "u8" else 0) if sw is not None else None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_sweep.json")
+    pmc = load_pmc(pmc_path, pmc_key, plan)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    pmc1 = load_pmc(pmc_path, pmc_key + "_stage1", plan) if fx_g else None
 
     if rank == 0:
-        plan = sw.info(1 if dtype == "u8" else 0) if sw is not None else None
         line = {
             "metric": "DM-trial samples*channels/sec (node) + % HBM roofline",
             "value": value,
@@ -532,9 +545,15 @@ def sweep_bench(args, cfg, rank, world, dev):
             "roofline": {"bound": "lds", "achieved": achieved, "peak": lds_roof,
                          "unit": "T adds/s", "frac": achieved / lds_roof if achieved else None,
                          "traffic": traffic,
-                         "traffic_source": ("profiles/pmc_sweep.json[%s] (separate rocprofv3 "
+                         "traffic_source": ("profiles/pmc_sweep.json[%s]: separate rocprofv3 "
                                             "--pmc FETCH_SIZE / WRITE_SIZE passes of this "
-                                            "command)" % pmc_key) if traffic else None,
+                                            "command, kernel %s, commit %s, source digest %s "
+                                            "(= this build)" % (pmc_key, pmc.get("kernel"),
+                                                                pmc.get("commit"),
+                                                                pmc.get("src_digest")))
+                         if traffic else "no PMC entry measured on this build (source digest / "
+                                         "plan mismatch): traffic not reported",
+                         "traffic_stage1": pmc1.get("hbm_bytes_per_launch") if pmc1 else None,
                          "kernel": ("pdd::k_sweep_il (factorised stage 2)" if fx_g
                                     else "pdd::k_sweep_il"), "kernel_ms_per_launch":
                              kern_ms / launches if launches else None,

@@ -127,6 +127,37 @@ def test_config3_sweep_oracle_rows(gpu):
     ds.close()
 
 
+def test_northstar_g2_plane(gpu):
+    """The north-star grid (4096 ch, 2048 DMs 0-1000, DDplan2b.py:168
+    arange grid spacing) at N = 2^18: the planner picks the factorised sweep
+    over groups of 2 channels (the per-lane staging instance of k_sweep_il),
+    its plane equals the channel-by-channel kernel bit for bit, and sampled
+    rows equal the oracle's per-trial channel sums."""
+    import torch
+    from oracle import spectra_oracle as orc
+    from pypulsar_amd import _lib
+    from pypulsar_amd.sweep import DMSweep
+    C, N, D = 4096, 1 << 18, 2048
+    freqs = band(C)
+    dms = np.linspace(0.0, 1000.0, D)
+    x = _u8(C, N, 13)
+    xd = torch.from_numpy(x).cuda()
+    sw = DMSweep(dms, freqs, DT, dtype="u8")
+    g, n_pat = sw.factor_info(_lib.U8)
+    assert g == 2 and n_pat > 0, (g, n_pat)
+    plane = sw(xd)
+    n_out = plane.shape[1]
+    assert n_out == N - 14504
+    ch = DMSweep(dms, freqs, DT, dtype="u8", factor=False)
+    assert ch.factor_info(_lib.U8)[0] == 0
+    assert torch.equal(ch(xd), plane)
+    ch.close()
+    rows = [0, 1, 683, 1023, 1024, 2046, 2047]
+    want = orc.sweep_rows_inside(x, orc.sweep_table(dms, freqs, DT)[rows], n_out)
+    np.testing.assert_array_equal(plane[rows].cpu().numpy().astype(np.float64), want)
+    sw.close()
+
+
 def test_config1_full_size_f32(gpu):
     """BASELINE configs[1] at its full size -- 1024 ch x 2^20 samples x 1024
     DMs (0-1000), float32: on integer data the float32 plane equals the exact

@@ -146,3 +146,38 @@ def test_streaming_search_equals_one_shot(gpu, nchunks, last, nplanes):
     key = lambda r: sorted(zip(r["row"], r["Sample"], r["Downfact"]))
     assert key(got) == key(want)
     np.testing.assert_array_equal(np.sort(got["Sigma"]), np.sort(want["Sigma"]))
+
+
+def test_search_snr_pinned_to_reference_smooth(gpu):
+    """Device search on the rows of tests/golden/golden_pulse.npz (already
+    chunk-normalised, float32 values) against the reference's own
+    Pulse.smooth (formats/pulse.py:217-241): every 1024-start window's best
+    S/N over the search widths equals the maximum of the reference's smoothed
+    profiles over the same starts (interior: Pulse.smooth[t + w//2]) within
+    1e-4, and the detections match."""
+    import os
+    import torch
+    from pypulsar_amd.search import SinglePulseSearch
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                             "golden_pulse.npz"), allow_pickle=False)
+    z = g["z"]
+    R, n = z.shape
+    widths = tuple(int(w) for w in g["widths"])
+    best = np.full((R, -(-n // 1024)), -np.inf)
+    for w in widths:
+        s = g["smooth_w%d" % w][:, w // 2:w // 2 + n - w + 1]    # start t -> Pulse.smooth[t + w//2]
+        pad = best.shape[1] * 1024 - s.shape[1]
+        s = np.concatenate([s, np.full((R, pad), -np.inf)], axis=1).reshape(R, -1, 1024)
+        best = np.maximum(best, s.max(axis=2))
+    thr = 5.0
+    sp = SinglePulseSearch(threshold=thr, widths=widths, detrendlen=1024)
+    got = sp(torch.from_numpy(z.astype(np.float32)).cuda(), dms=np.arange(R) * 1.0, dt=1e-3)
+    gg = {(int(r), int(t) // 1024): float(s) for r, t, s in zip(got["row"], got["Sample"], got["Sigma"])}
+    want = {(r, k): best[r, k] for r in range(R) for k in range(best.shape[1]) if best[r, k] >= thr}
+    assert len(want) >= R
+    for key in set(gg) | set(want):
+        if key in gg and key in want:
+            assert abs(gg[key] - want[key]) <= 1e-4 * max(1.0, abs(want[key])), (key, gg[key], want[key])
+        else:
+            s = gg.get(key, want.get(key))
+            assert abs(s - thr) <= 1e-4 * thr, (key, s)

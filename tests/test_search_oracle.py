@@ -83,3 +83,39 @@ def test_widths_validation():
         search._widths([0, 1])
     with pytest.raises(AssertionError):
         search._widths(list(range(1, 40)))
+
+
+def _golden_pulse():
+    import os
+    return np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                "golden_pulse.npz"), allow_pickle=False)
+
+
+def test_boxcar_pinned_to_reference_pulse_smooth():
+    """The search's boxcar (so.boxcar_snr) == the reference's Pulse.smooth
+    (formats/pulse.py:217-241, run by tests/golden/make_golden_pulse.py) on
+    every start whose boxcar lies inside the row: Pulse.smooth's output at
+    t + w//2 is sum(z[t:t+w]) * float32(1/sqrt(w)) (convolve 'same' centres
+    the top-hat there; the wrap padding only reaches the edges).  Tolerance:
+    1e-6 relative -- the reference's kernel is float32(1/sqrt(w))."""
+    g = _golden_pulse()
+    z = g["z"]
+    n = z.shape[1]
+    for w in g["widths"]:
+        w = int(w)
+        ref = g["smooth_w%d" % w][:, w // 2:w // 2 + n - w + 1]
+        got = so.boxcar_snr(z, w)
+        assert got.shape == ref.shape
+        np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-9 * np.abs(ref).max())
+
+
+def test_downsample_pinned_to_reference_pulse_downsample():
+    """Pulse.downsample (pulse.py:177-195, py2 division restored) == the
+    oracle's Spectra.downsample restatement on one series (co-adds of f
+    adjacent bins), bit for bit."""
+    from oracle import spectra_oracle as orc
+    g = _golden_pulse()
+    x = g["ds_x"]
+    for f in (1, 2, 3, 4, 8, 16):
+        got, _ = orc.downsample(x, 64e-6, f)
+        np.testing.assert_array_equal(got, g["ds_f%d" % f])
