@@ -58,13 +58,13 @@ PEAK_ADD_T = VALU_LANE_OPS_T * 2   # v_pk_add_f32 / v_add_u32 on packed u16: 2 a
 CONFIGS = {
     # BASELINE.json configs[3] (the metric's configuration): DM-sharded node sweep
     "config3": dict(C=4096, N=1 << 22, D=4096, dm_lo=0.0, dm_hi=1000.0, dtype="u8",
-                    mode="dmshard", cpu=(4096, 1 << 17, 12), baseline_index=3),
+                    mode="auto", cpu=(4096, 1 << 17, 12), baseline_index=3),
     # BASELINE.json configs[1]: single-GPU brute-force sweep, float32
     "config2": dict(C=1024, N=1 << 20, D=1024, dm_lo=0.0, dm_hi=1000.0, dtype="f32",
                     mode="timeblock", cpu=(1024, 1 << 20, 3), baseline_index=1),
     # north-star single-GPU target (4096 ch x 2048 DM x 2^22)
     "northstar": dict(C=4096, N=1 << 22, D=2048, dm_lo=0.0, dm_hi=1000.0, dtype="u8",
-                      mode="dmshard", cpu=(4096, 1 << 17, 12), baseline_index=None),
+                      mode="auto", cpu=(4096, 1 << 17, 12), baseline_index=None),
     "small": dict(C=256, N=1 << 18, D=256, dm_lo=0.0, dm_hi=500.0, dtype="f32",
                   mode="timeblock", cpu=(256, 1 << 18, 8), baseline_index=None),
     # BASELINE.json configs[4]: streaming u8 blocks, zero-DM + ds 2 + 2048 DMs
@@ -277,7 +277,11 @@ def main():
     ap.add_argument("--config", default="config3", choices=sorted(CONFIGS))
     ap.add_argument("--block", type=int, default=None, help="stream: spectra per block")
     ap.add_argument("--dtype", default=None, choices=["f32", "u8"])
-    ap.add_argument("--mode", default=None, choices=["timeblock", "dmshard"])
+    ap.add_argument("--mode", default=None, choices=["timeblock", "dmshard", "timeshard", "auto"],
+                    help="config3/northstar: dmshard (DM slices, RCCL all-gathers), timeshard "
+                         "(column ranges of the same block, no collective) or auto (the "
+                         "default: dmshard at N = 1, timeshard at N > 1 -- bench.py "
+                         "--rehearse 8 measures both, DESIGN.md §5)")
     ap.add_argument("--batches", type=int, default=None,
                     help="dmshard: time batches per step (default 1 on one GPU, 4 otherwise)")
     ap.add_argument("--gather", action="store_true",
@@ -333,6 +337,8 @@ def main():
         return search_bench(args, cfg, rank, world, dev)
     if args.config == "ops":
         return ops_bench(args, cfg, rank, world, dev)
+    if args.rehearse and (args.mode or "dmshard") == "timeshard":
+        return rehearse_timeshard(args, cfg, dev)
     if args.rehearse:
         return rehearse_bench(args, cfg, dev)
     return sweep_bench(args, cfg, rank, world, dev)
@@ -340,13 +346,15 @@ def main():
 
 def sweep_bench(args, cfg, rank, world, dev):
     from pypulsar_amd.sweep import DMSweep
-    from pypulsar_amd.sharding import DMShardedSweep, trial_work
+    from pypulsar_amd.sharding import DMShardedSweep, TimeShardedSweep, trial_work
     big = cfg["C"] * cfg["N"] >= (1 << 34)
     steps = args.steps if args.steps is not None else (5 if big else 10)
     warmup = args.warmup if args.warmup is not None else (1 if big else 3)
     C, N, D = cfg["C"], cfg["N"], cfg["D"]
     dtype = args.dtype or cfg["dtype"]
     mode = args.mode or cfg["mode"]
+    if mode == "auto":
+        mode = "dmshard" if world == 1 else "timeshard"
     dt = 64e-6
     freqs = band(C)
     dms_all = np.linspace(cfg["dm_lo"], cfg["dm_hi"], D)
@@ -367,13 +375,29 @@ def sweep_bench(args, cfg, rank, world, dev):
         n_r = N // (nb * world)
         part = synth_block(nb * n_r, C, 1000 + rank, dtype, dev).view(nb, n_r, C)
         sw, rows, n_out = ds.sw, ds.rows, ds.n_out
+        cols_rank, n_in_rank = n_out, N
 
         def step():
             return ds(part)
+    elif mode == "timeshard":
+        # column ranges of the same block: rank r holds its own input spectra
+        # (columns + the max-delay overlap, time-major, its own H2D), no
+        # collective (pypulsar_amd.sharding.TimeShardedSweep)
+        ts = TimeShardedSweep(dms_all, freqs, dt, N, dtype=tdt, gather=args.gather, device=dev,
+                              factor=_factor_arg(args))
+        log("rank %d: plane columns [%d, %d) of %d, input spectra [%d, %d)"
+            % (rank, ts.a, ts.b, ts.n_out, ts.in_lo, ts.in_hi))
+        part = synth_block(ts.n_in, C, 1000 + rank, dtype, dev)   # [n_in, C] file order
+        sw, rows, n_out = ts.sw, D, ts.n_out
+        cols_rank, n_in_rank = ts.cols, ts.n_in
+
+        def step():
+            return ts(part)
     else:
         x = synth_block(C, N, 1000 + rank, dtype, dev)
         sw = DMSweep(dms_all, freqs, dt, dtype=dtype, factor=_factor_arg(args))
         rows, n_out = D, sw.n_out(N)
+        cols_rank, n_in_rank = n_out, N
         plane = torch.empty((D, n_out), dtype=torch.float32, device=dev)
 
         def step():
@@ -476,7 +500,7 @@ def sweep_bench(args, cfg, rank, world, dev):
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    adds_rank_step = rows * n_out * C            # one add per samp*ch*DM on this rank
+    adds_rank_step = rows * cols_rank * C        # one add per samp*ch*DM on this rank
     units_all = D * n_out * C * (world if mode == "timeblock" else 1)
     value = units_all * steps / el
     s_in = 1 if dtype == "u8" else 4
@@ -484,7 +508,7 @@ def sweep_bench(args, cfg, rank, world, dev):
     # pattern sample per (trial, group of fx channels), so its own adds are
     # C / fx per samp*DM; the algorithmic rate is reported beside them
     fx_g, fx_pat = sw.factor_info(1) if (sw is not None and dtype == "u8") else (0, 0)
-    kern_adds_step = rows * n_out * (C // fx_g) if fx_g else adds_rank_step
+    kern_adds_step = rows * cols_rank * (C // fx_g) if fx_g else adds_rank_step
     achieved = kern_adds_step * steps / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else None
     effective = adds_rank_step * steps / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else None
     # LDS roof (the binding one): ds_read_b128 at 256 B/clk/CU
@@ -494,7 +518,7 @@ def sweep_bench(args, cfg, rank, world, dev):
     # v_add3_u32 lane-op (4 adds); f32 quarters two samples per v_pk_add_f32
     valu_adds = 4 if dtype == "u8" else 2
     valu_roof = VALU_LANE_OPS_T * valu_adds
-    uniq_bytes = C * N * s_in + rows * n_out * 4
+    uniq_bytes = C * n_in_rank * s_in + rows * cols_rank * 4
     k_s = kern_ms * 1e-3 / steps if kern_ms > 0 else None
     # keys of profiles/pmc_sweep.json (scripts/collect_profiles_r3.py): the
     # default configs[3] line (factorised), its channel-kernel line, ...
@@ -534,10 +558,16 @@ def sweep_bench(args, cfg, rank, world, dev):
                                       "slices, %d batch(es), planes %s)"
                                       % (nb, "gathered to rank 0" if args.gather else
                                          "resident per rank") if mode == "dmshard" else
-                                      ", every rank its own block"),
+                                      (", time-sharded (each rank a contiguous range of plane "
+                                       "columns from its own input spectra + the max-delay "
+                                       "overlap, no collective, planes %s)"
+                                       % ("gathered to rank 0" if args.gather else
+                                          "resident per rank") if mode == "timeshard" else
+                                       ", every rank its own block")),
                        "config_name": args.config, "channels": C, "samples": N, "dm_trials": D,
-                       "n_out": n_out, "parallelism": "%s%d" % ("tb" if mode == "timeblock"
-                                                                else "dm", world),
+                       "n_out": n_out, "mode": mode,
+                       "parallelism": "%s%d" % ({"timeblock": "tb", "timeshard": "ts"}
+                                                .get(mode, "dm"), world),
                        "rccl_world_size": rccl_world, "plan": plan,
                        "method": ("exact factorisation over groups of %d channels (%d pattern "
                                   "series; plane bit-identical to the channel-by-channel sum)"
@@ -594,7 +624,7 @@ def sweep_bench(args, cfg, rank, world, dev):
             line["end_to_end_pcie"] = e2e
         if world == 1 and not args.no_cpu_baseline:
             del step
-            if mode == "dmshard":
+            if mode in ("dmshard", "timeshard"):
                 del part
             else:
                 del x
@@ -697,6 +727,79 @@ def rehearse_bench(args, cfg, dev):
     from pypulsar_amd.delays import sweep_table
     n_out = N - int(sweep_table(dms[-1:], freqs, dt).max())
     line["predicted_value_at_W"] = D * n_out * C / (tmax * 1e-3)
+    print(json.dumps(line), flush=True)
+
+
+def rehearse_timeshard(args, cfg, dev):
+    """The W-rank TIME-sharded step rehearsed on ONE GPU: first the whole
+    block as one rank (W = 1: the whole plane), then rank r = 0..W-1 exactly
+    as it runs in a W-GPU job (TimeShardedSweep(world=W, rank=r): corner turn
+    of its own input spectra -- its plane columns plus the max-delay overlap
+    -- and the sweep of the whole grid over its columns).  There is no
+    exchange to replace: the rank's compute IS its W-GPU step (inputs
+    resident).  Reports per-rank step and sweep-kernel times and the
+    predicted efficiency t(1 GPU) / (W * max_r t_r)."""
+    from pypulsar_amd.sharding import TimeShardedSweep
+    W = args.rehearse
+    C, N, D = cfg["C"], cfg["N"], cfg["D"]
+    dtype = args.dtype or cfg["dtype"]
+    tdt = torch.uint8 if dtype == "u8" else torch.float32
+    dt = 64e-6
+    freqs = band(C)
+    dms = np.linspace(cfg["dm_lo"], cfg["dm_hi"], D)
+    steps = args.steps if args.steps is not None else 3
+    warmup = args.warmup if args.warmup is not None else 1
+    block = synth_block(N, C, 1000, dtype, dev)            # time-major [N, C], file order
+
+    def timed(ts, part):
+        for _ in range(warmup):
+            ts(part)
+        torch.cuda.synchronize()
+        ts.sw.set_timing(True)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            ts(part)
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) / steps * 1e3
+        kms, launches = ts.sw.timing_read()
+        ts.sw.set_timing(False)
+        return el, kms / steps, launches // steps
+
+    res = []
+    for w, r in [(1, 0)] + [(W, r) for r in range(W)]:
+        ts = TimeShardedSweep(dms, freqs, dt, N, dtype=tdt, world=w, rank=r, device=dev,
+                              factor=_factor_arg(args))
+        lo, hi = ts.input_range()
+        t, k, l = timed(ts, block[lo:hi])
+        g, npat = ts.sw.factor_info(1 if dtype == "u8" else 0)
+        res.append({"rank": r, "world": w, "cols": [ts.a, ts.b], "input": [lo, hi],
+                    "step_ms": t, "sweep_kernel_ms": k, "launches": l, "fx": [g, npat]})
+        log("rehearse timeshard: W=%d rank %d columns [%d, %d) step %.1f ms (sweep %.1f ms, "
+            "%d launches)" % (w, r, ts.a, ts.b, t, k, l))
+        n_out = ts.n_out
+        ts.close()
+        del ts
+        torch.cuda.empty_cache()
+    one, ranks = res[0], res[1:]
+    tmax = max(x["step_ms"] for x in ranks)
+    line = {
+        "metric": "rehearsal of the %d-GPU time-sharded step on one GPU" % W,
+        "value": one["step_ms"] / (W * tmax),
+        "unit": "predicted efficiency t1 / (W * max_r t_r)",
+        "n_gpus": 1, "rehearsed_world": W, "steps": steps, "warmup": warmup,
+        "higher_is_better": True, "dtype": dtype,
+        "config": {"workload": "%d ch x 2^%d x %d DM (%g-%g pc/cc), time-sharded: rank r sweeps "
+                               "plane columns [a_r, b_r) from input spectra [a_r, b_r + max delay)"
+                               % (C, int(np.log2(N)), D, cfg["dm_lo"], cfg["dm_hi"]),
+                   "config_name": args.config, "mode": "timeshard"},
+        "one_gpu": one, "ranks": ranks,
+        "max_rank_step_ms": tmax,
+        "mean_rank_step_ms": float(np.mean([x["step_ms"] for x in ranks])),
+        "predicted_step_ms_at_W": tmax,
+        "predicted_value_at_W": D * n_out * C / (tmax * 1e-3),
+        "note": "no exchange exists in this partition (each rank's input spectra are its own "
+                "H2D); the rank steps are the W-GPU step's per-rank compute exactly",
+    }
     print(json.dumps(line), flush=True)
 
 

@@ -358,6 +358,127 @@ class DMShardedSweep(object):
             self.sw = None
 
 
+def timeshard_edges(n_out, world, align=1024):
+    """Plane column edges of a time-sharded sweep: ``world`` ranges of
+    (nearly) equal width, interior edges on multiples of ``align`` (the
+    sweep's time tile: 1024 samples for both the u16-eighths and the float32
+    quarters tiling), so no rank sweeps a partial tile except the last."""
+    edges = [0]
+    for r in range(1, world):
+        e = int(round(n_out * r / world / align)) * align
+        edges.append(min(max(e, edges[-1]), n_out))
+    edges.append(int(n_out))
+    return edges
+
+
+class TimeShardedSweep(object):
+    """Time-sharded sweep of ONE filterbank block across the ranks (SURVEY.md
+    §8(e) 2, strong scaling: the block and the grid are fixed, each of W
+    GPUs owns a contiguous range of plane COLUMNS and sweeps the whole DM
+    grid over it).  No collective: rank r reads input spectra
+    [a_r, b_r + max_bin) -- its columns plus an overlap of the largest delay
+    (14 504 samples at configs[3], 2.8% of 2^22 / 8) -- straight from the
+    file / host (its own H2D), corner-turns them and sweeps columns
+    [a_r, b_r) of the one-shot plane
+        plane[d][t] = sum_c X(c, t + bins[d][c]),  t < n_out = N - max bin
+    (Spectra.dedisperse(dms[d], trim=True) + channel sum, formats/spectra.py
+    :229-260 + bin/waterfaller.py:140).  Every trial's delays are >= 0 and
+    t + bins <= b_r - 1 + max_bin < in_hi, so no pad is read and the ranks'
+    column blocks concatenate to the one-shot plane bit for bit.
+
+    Why a second partition: the exact factorised sweep pays a
+    stage 1 per pattern over the whole time range; under DM sharding a rank's
+    trial slice still uses about a third of the grid's patterns at W = 8, so
+    stage 1 does not shrink with W.  Time sharding keeps every rank's work
+    exactly 1/W of the one-GPU step plus the overlap.
+
+    ``part``: this rank's [n_in, C] time-major input (file order).  Planes
+    stay resident; ``gather=True`` sends each rank's [D, cols] block to
+    ``dst``, which places it in its full [D, n_out] plane.  ``world, rank``
+    without a process group: the rehearsal (the rank's compute is the same,
+    there is nothing to replace).  ``to_cm`` / ``sweep_fn(x, out, n_cols)``
+    are injected by the CPU tests."""
+
+    def __init__(self, dms, freqs, dt, N, dtype=torch.uint8, world=None, rank=None, gather=False,
+                 dst=0, group=None, device=None, to_cm=None, sweep_fn=None, factor=True,
+                 align=1024):
+        from . import delays as _delays
+        self.group = group
+        if world is not None:
+            self.world, self.rank = int(world), int(rank)
+            assert 0 <= self.rank < self.world
+            assert not gather, "a rehearsal has no plane gather (one device)"
+        else:
+            self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+            self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.dms = np.asarray(dms, dtype=np.float64)
+        self.freqs = np.asarray(freqs, dtype=np.float64)
+        self.C, self.N, self.D = len(self.freqs), int(N), len(self.dms)
+        self.dt, self.dtype = dt, dtype
+        self.device = torch.device("cpu") if device is None else torch.device(device)
+        tab = _delays.sweep_table(self.dms, self.freqs, dt)
+        assert tab.size == 0 or tab.min() >= 0, "time-sharded sweep expects delays >= 0"
+        self.max_bin = int(tab.max()) if tab.size else 0
+        self.n_out = self.N - self.max_bin
+        assert self.n_out > 0
+        self.edges = timeshard_edges(self.n_out, self.world, align)
+        self.a, self.b = self.edges[self.rank], self.edges[self.rank + 1]
+        self.cols = self.b - self.a
+        self.in_lo, self.in_hi = self.a, self.b + self.max_bin   # input spectra of this rank
+        self.n_in = self.in_hi - self.in_lo
+        self.gather, self.dst = bool(gather), dst
+        self.x = torch.empty((self.C, self.n_in), dtype=dtype, device=self.device)
+        self.full = None
+        if self.gather and self.rank == self.dst:
+            self.full = torch.empty((self.D, self.n_out), dtype=torch.float32, device=self.device)
+            self.recv = {r: torch.empty((self.D, self.edges[r + 1] - self.edges[r]),
+                                        dtype=torch.float32, device=self.device)
+                         for r in range(self.world) if r != self.dst}
+        self.out = torch.empty((self.D, self.cols), dtype=torch.float32, device=self.device)
+        self.to_cm = to_cm if to_cm is not None else _corner_turn
+        self.sw = None
+        if sweep_fn is None:
+            from .sweep import DMSweep
+            self.sw = DMSweep(self.dms, self.freqs, dt,
+                              dtype="u8" if dtype == torch.uint8 else "f32", factor=factor)
+
+            def sweep_fn(x, out, n_cols):
+                self.sw(x, out=out, n_out=n_cols)
+        self.sweep_fn = sweep_fn
+
+    def input_range(self, rank=None):
+        """[lo, hi) input spectra of ``rank`` (default this rank)."""
+        r = self.rank if rank is None else rank
+        return self.edges[r], self.edges[r + 1] + self.max_bin
+
+    def __call__(self, part):
+        """One step: corner turn of this rank's [n_in, C] spectra, sweep of
+        its columns (and, with ``gather``, the blocks to ``dst``).  Returns
+        this rank's [D, cols] plane (``dst`` with gather: the full plane)."""
+        assert tuple(part.shape) == (self.n_in, self.C) and part.dtype == self.dtype
+        self.to_cm(part, self.x)
+        if self.cols:
+            self.sweep_fn(self.x, self.out, self.cols)
+        if not self.gather or self.world == 1:
+            return self.out
+        if self.rank != self.dst:
+            if self.cols:
+                dist.send(self.out, self.dst, group=self.group)
+            return self.out
+        works = [(r, dist.irecv(buf, r, group=self.group)) for r, buf in self.recv.items()
+                 if buf.shape[1]]
+        self.full[:, self.a:self.b] = self.out
+        for r, w in works:
+            w.wait()
+            self.full[:, self.edges[r]:self.edges[r + 1]] = self.recv[r]
+        return self.full
+
+    def close(self):
+        if self.sw is not None:
+            self.sw.close()
+            self.sw = None
+
+
 def split_block(block_tc, n_batches, world, rank):
     """This rank's ``part`` of a time-major [N, C] block for DMShardedSweep:
     [n_batches, N/(n_batches*world), C] (a copy)."""

@@ -158,6 +158,41 @@ def test_northstar_g2_plane(gpu):
     sw.close()
 
 
+def test_config3_timeshard_8_ranks(gpu):
+    """The 8-rank TIME-sharded configs[3] step (TimeShardedSweep(world=8,
+    rank=r), bench.py's N > 1 default) at N = 2^18 on one GPU: each rank
+    corner-turns its own input spectra (its plane columns + the max-delay
+    overlap) and sweeps the whole 4096-DM grid over its columns with its own
+    (factorised) plan; the 8 column blocks concatenate to the one-shot plane
+    bit for bit, and sampled rows equal the oracle."""
+    import torch
+    from oracle import spectra_oracle as orc
+    from pypulsar_amd.sharding import TimeShardedSweep
+    from pypulsar_amd.sweep import DMSweep
+    C, N, D, W = 4096, 1 << 18, 4096, 8
+    freqs = band(C)
+    dms = np.linspace(0.0, 1000.0, D)
+    x = _u8(C, N, 17)
+    xd = torch.from_numpy(x).cuda()
+    sw = DMSweep(dms, freqs, DT, dtype="u8")
+    plane = sw(xd)
+    sw.close()
+    block = xd.t().contiguous()                      # time-major [N, C], file order
+    cols = []
+    for r in range(W):
+        ts = TimeShardedSweep(dms, freqs, DT, N, dtype=torch.uint8, world=W, rank=r, device="cuda")
+        lo, hi = ts.input_range()
+        assert hi - lo == ts.cols + 14504 and ts.a % 1024 == 0
+        cols.append(ts(block[lo:hi]).clone())
+        ts.close()
+    got = torch.cat(cols, dim=1)
+    assert got.shape == plane.shape
+    assert torch.equal(got, plane)
+    rows = [0, 2047, 4095]
+    want = orc.sweep_rows_inside(x, orc.sweep_table(dms, freqs, DT)[rows], plane.shape[1])
+    np.testing.assert_array_equal(got[rows].cpu().numpy().astype(np.float64), want)
+
+
 def test_config1_full_size_f32(gpu):
     """BASELINE configs[1] at its full size -- 1024 ch x 2^20 samples x 1024
     DMs (0-1000), float32: on integer data the float32 plane equals the exact

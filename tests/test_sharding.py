@@ -94,6 +94,24 @@ def _worker(rank, world, port, q):
             xv = x[:, x_off:x_off + n_cols + int(tab.max())]
             out.copy_(torch.from_numpy(orc.sweep_plane(xv.numpy().astype(np.float64), tab,
                                                        n_out=n_cols).astype(np.float32)))
+        # time sharding (TimeShardedSweep): rank r sweeps plane columns
+        # [a_r, b_r) of the whole grid from its own input spectra, no
+        # collective; resident blocks, or gathered to rank 0
+        def ts_sweep(x, out, n_cols):
+            tab = orc.sweep_table(dms, freqs, DT)
+            out.copy_(torch.from_numpy(orc.sweep_plane(x.numpy().astype(np.float64), tab,
+                                                       n_out=n_cols).astype(np.float32)))
+        blk = torch.from_numpy(_data(C, NB).T.copy())
+        ts_res = {}
+        for gather in (False, True):
+            ts = sharding.TimeShardedSweep(dms, freqs, DT, NB, dtype=torch.float32, gather=gather,
+                                           to_cm=to_cm, sweep_fn=ts_sweep, align=64)
+            lo, hi = ts.input_range()
+            for _ in range(2):
+                out = ts(blk[lo:hi].contiguous())
+            ts_res[gather] = (ts.a, out.numpy().copy())
+        tsr = [None] * world
+        dist.all_gather_object(tsr, ts_res[False])
         res = {}
         # NB = 2400 splits into 2 batches x world slices of 600 or 400 spectra
         # (time-major path); NBP = 4096 into power-of-two slices (pieces path)
@@ -129,6 +147,8 @@ def _worker(rank, world, port, q):
             q.put(("dm", plane.numpy()))
             q.put(("tb", np.concatenate(parts, axis=1)))
             q.put(("sp", cands))
+            q.put(("ts", np.concatenate([p for _, p in sorted(tsr, key=lambda a: a[0])], axis=1)))
+            q.put(("tsg", ts_res[True][1]))
     finally:
         dist.destroy_process_group()
 
@@ -142,7 +162,7 @@ def test_sharded_sweeps_equal_one_shot(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=240) for _ in range(8))
+    got = dict(q.get(timeout=240) for _ in range(10))
     for p in procs:
         p.join(timeout=240)
         assert p.exitcode == 0
@@ -162,6 +182,8 @@ def test_sharded_sweeps_equal_one_shot(world):
         want_p = orc.sweep_plane(_data(C, 4096).astype(np.float64), tab)
         np.testing.assert_array_equal(got["agp"].astype(np.float64), want_p)
         np.testing.assert_array_equal(got["aggp"].astype(np.float64), want_p)
+    np.testing.assert_array_equal(got["ts"].astype(np.float64), want_b)
+    np.testing.assert_array_equal(got["tsg"].astype(np.float64), want_b)
     # sharded search == search of the one-shot plane
     from oracle import search_oracle as so
     xs = _data(C, N)
@@ -231,3 +253,43 @@ def test_rehearsal_ranks_stack_to_one_shot(world, nbk, pieces):
         rows.append(ds.plane().numpy())
     want = orc.sweep_plane(_data(C, nbk).astype(np.float64), tab)
     np.testing.assert_array_equal(np.concatenate(rows).astype(np.float64), want)
+
+
+def test_timeshard_edges():
+    e = sharding.timeshard_edges(4179800, 8)
+    assert e[0] == 0 and e[-1] == 4179800 and len(e) == 9
+    assert all(x % 1024 == 0 for x in e[1:-1])
+    w = np.diff(e)
+    assert w.max() - w.min() <= 1024 + 4179800 % 1024
+    assert sharding.timeshard_edges(100, 4, align=64) == [0, 0, 64, 64, 100]
+
+
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_timeshard_rehearsal_ranks_concatenate_to_one_shot(world):
+    """TimeShardedSweep(world=W, rank=r) on one process: each rank's corner
+    turn of its own input spectra (columns + the max-delay overlap) and
+    sweep of its columns; the W column blocks concatenate to the one-shot
+    plane (host logic of bench.py --rehearse W --mode timeshard)."""
+    from oracle import spectra_oracle as orc
+    C, N = 16, 3000
+    freqs = _band(C)
+    dms = np.linspace(0.0, 40.0, 11)
+    tab = orc.sweep_table(dms, freqs, DT)
+
+    def to_cm(src_tc, dst_cm):
+        dst_cm.copy_(src_tc.t())
+
+    def sweep_fn(x, out, n_cols):
+        out.copy_(torch.from_numpy(orc.sweep_plane(x.numpy().astype(np.float64), tab,
+                                                   n_out=n_cols).astype(np.float32)))
+
+    block = torch.from_numpy(_data(C, N).T.copy())
+    cols = []
+    for r in range(world):
+        ts = sharding.TimeShardedSweep(dms, freqs, DT, N, dtype=torch.float32, world=world, rank=r,
+                                       to_cm=to_cm, sweep_fn=sweep_fn, align=64)
+        lo, hi = ts.input_range()
+        assert hi - lo == ts.cols + int(tab.max()) and hi <= N
+        cols.append(ts(block[lo:hi].contiguous()).numpy().copy())
+    want = orc.sweep_plane(_data(C, N).astype(np.float64), tab)
+    np.testing.assert_array_equal(np.concatenate(cols, axis=1).astype(np.float64), want)
