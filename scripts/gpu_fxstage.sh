@@ -13,6 +13,6 @@ for run in ${RUNS:-"config3:4:1" "config3:4:2" "northstar:2:0" "northstar:2:2" "
   echo "$c g=$g stage=$st: $(k $O/b.json)"
 done
 for st in ${RUNT:-2}; do
-  PDD_FX_STAGE=$st timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "factor or config or sweep" > $O/pytest_$st.log 2>&1
+  PDD_FX_STAGE=$st timeout -k 10 600 python -u -m pytest -m gpu -x -q --timeout 200 --timeout-method thread ${TF:-tests} -k "${TK:-factor or config or sweep}" > $O/pytest_$st.log 2>&1
   rc=$?; echo "tests stage=$st: $(tail -1 $O/pytest_$st.log)"; [ $rc -eq 0 ] || exit $rc
 done
