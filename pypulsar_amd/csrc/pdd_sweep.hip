@@ -1056,7 +1056,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const int b = k % NBUF;
     const int nw = __builtin_amdgcn_readlane(rec.w, 0) >> 20;
     int n = 0;
-    if constexpr (FXS == 1) {
+    if constexpr (FXS & 1) {
       // lane i = window i: its source, LDS address and piece count in one
       // pass, then this loader's windows (i = first mod step) from SGPRs
       const uint64_t sv = (uint64_t)(R + (int64_t)(rec.w & 0xfffff) * nR + (t0 + rec.x - lo));
@@ -1116,6 +1116,10 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       return n;
     };
     int4 rec_next = fx_rec(0);
+    // FXS 2: the records are loaded two chunks ahead; the load issued after a
+    // chunk's DMAs stays in flight through the wait before the next barrier
+    int4 rec_next2 = (FX && (FXS & 2)) ? fx_rec(1) : make_int4(0, 0, 0, 0);
+    int rec_tail = 0;  // FXS 2: a record load issued after the last chunk's DMAs
     auto issue_samples = [&](int k) -> int {
       if (dbg & 1) return 0;
       if constexpr (FX) {
@@ -1123,6 +1127,10 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
         // it is the one this iteration already did); load chunk k + 1's now
         const int4 rec = rec_next;
         int n = fx_issue(k, rec, lw, NLW);
+        if constexpr ((FXS & 2) != 0) {
+          rec_next = rec_next2;  // (chunk k + 2's record: rec_ahead, after the metadata)
+          return n;
+        }
         if (k + 1 < nchunk) {
           rec_next = fx_rec(k + 1);
           ++n;  // rides on the counted vmcnt
@@ -1158,6 +1166,20 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       }
       return n;
     };
+    // FXS 2: chunk c + 2's record, issued after chunk c's DMAs and the
+    // metadata DMAs (the youngest operation: the wait before the next
+    // barrier leaves it in flight)
+    auto rec_ahead = [&](int c) -> int {
+      rec_tail = 0;
+      if constexpr (FX && (FXS & 2)) {
+        if (c + 2 < nchunk && !(dbg & 1)) {
+          rec_next2 = fx_rec(c + 2);
+          rec_tail = 1;
+          return 1;
+        }
+      }
+      return 0;
+    };
     for (int k = 0; k < MA; ++k) issue_meta(k);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // prologue: every ring's first MA slots landed
@@ -1169,13 +1191,13 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     for (int s2 = 0; s2 < NBUF - 1; ++s2) {
 #pragma unroll
       for (int i = NBUF - 1; i > 0; --i) hist[i] = hist[i - 1];
-      hist[0] = s2 < nchunk ? issue_samples(s2) : 0;
+      hist[0] = s2 < nchunk ? issue_samples(s2) + rec_ahead(s2) : 0;
     }
     uint64_t ts_poll = 0, ts_issue = 0, ts_wait = 0, tA = 0, tB = 0;
     for (int k = 0; k < nchunk; ++k) {
       // retire chunk k (and everything older); the NBUF-2 younger chunks stay in flight
       if (stamps) tA = __builtin_amdgcn_s_memtime();
-      int younger = 0;
+      int younger = (FX && (FXS & 2)) ? rec_tail : 0;
 #pragma unroll
       for (int i = 0; i < NBUF - 2; ++i) younger += hist[i];
       wait_vmcnt(younger);
@@ -1190,6 +1212,8 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       // records (it cannot see the DMAs) lands before any DMA of this iteration
       int n = k + NBUF - 1 < nchunk ? issue_samples(k + NBUF - 1) : 0;
       n += issue_meta(k + MA);
+      if (k + NBUF - 1 < nchunk) n += rec_ahead(k + NBUF - 1);
+      else rec_tail = 0;
 #pragma unroll
       for (int i = NBUF - 1; i > 0; --i) hist[i] = hist[i - 1];
       hist[0] = n;
@@ -1499,8 +1523,15 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false, int fxs = 0)
     // (the staging form is a template parameter: a runtime switch between
     // the two cost the north star's per-lane form 25%)
     if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
-      return fxs == 1 ? k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 1>
-                      : k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 0>;
+      switch (fxs) {
+#ifdef PDD_SWEEP_DEV
+        // the other staging forms, for timing comparisons (PDD_FX_STAGE)
+        case 0: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 0>;
+        case 1: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 1>;
+        case 2: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 2>;
+#endif
+        default: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 3>;
+      }
     return nullptr;
   }
 #define IL(NCW_, NLW_, CC_, NB_)                                                              \
@@ -1561,15 +1592,19 @@ static int debug_flags() {
   return 0;
 #endif
 }
-// Factorised staging: the loaders' per-window work from SGPRs (lane i
-// computes window i's addresses once per chunk; each loader walks only its
-// own windows) for groups of 4, whose stage 2 is loader-bound; groups of 2
-// keep the per-lane address form (profiles/r3_staging_probe.txt section 8).
+// Factorised staging form (k_sweep_il's FXS): bit 0 -- the loaders' per-window
+// work from SGPRs (lane i computes window i's addresses once per chunk; each
+// loader walks only its own windows, saddr-form DMAs); bit 1 -- the chunks'
+// window records loaded two chunks ahead (their load latency off the
+// per-chunk barrier path).  Round 4 (dev builds, same box, kernel ms per
+// launch; configs[3] g 4 / north star g 2): 1: 74.0 / 106.9 (round 3), 0:
+// - / 100.8, 2: 86.8 / 111.1, 3: 68.0 / 97.6 -> 3 for both group sizes.
 static int fx_stage_for(int g) {
+  (void)g;
 #ifdef PDD_SWEEP_DEV
   if (const char* e = getenv("PDD_FX_STAGE")) return atoi(e);
 #endif
-  return g == 4 ? 1 : 0;
+  return 3;
 }
 static int forced_variant() {
 #ifdef PDD_SWEEP_DEV
