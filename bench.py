@@ -507,7 +507,7 @@ def sweep_bench(args, cfg, rank, world, dev):
     # exact factorised 8-bit sweep: the kernel adds one
     # pattern sample per (trial, group of fx channels), so its own adds are
     # C / fx per samp*DM; the algorithmic rate is reported beside them
-    fx_g, fx_pat = sw.factor_info(1) if (sw is not None and dtype == "u8") else (0, 0)
+    fx_g, fx_pat = sw.factor_info(1 if dtype == "u8" else 0) if sw is not None else (0, 0)
     kern_adds_step = rows * cols_rank * (C // fx_g) if fx_g else adds_rank_step
     achieved = kern_adds_step * steps / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else None
     effective = adds_rank_step * steps / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else None
@@ -594,11 +594,12 @@ def sweep_bench(args, cfg, rank, world, dev):
                          "effective_units_T_per_s": effective,
                          "note": ("factorised stage 2: one add per samp*DM*(group of %d "
                                   "channels), each reading its pattern sample from the LDS image "
-                                  "(ds_read_b128: 8 samples per 16 B at 256 B/clk/CU = the peak, "
+                                  "(ds_read_b128: %d samples per 16 B at 256 B/clk/CU = the peak, "
                                   "in adds/s); the tile is bound by staging the pattern windows "
                                   "(LDS-DMA), so the LDS-read fraction is low by construction; "
                                   "effective_units_T_per_s = samp*ch*DM per second of this "
-                                  "kernel (DESIGN.md §3)" % fx_g) if fx_g else
+                                  "kernel (DESIGN.md §3-4)" % (fx_g, 8 if dtype == "u8" else 4))
+                         if fx_g else
                                  ("one add per samp*ch*DM, no MFMA-shaped work; every add reads "
                                   "its sample from the LDS image (ds_read_b128: %d samples per 16 B "
                                   "at 256 B/clk/CU = the peak, in adds/s), which binds; the VALU "

@@ -781,6 +781,63 @@ __global__ __launch_bounds__(256) void k_fx_patterns_x(const InT* __restrict__ x
   }
 }
 
+// Stage 1 of factorised float32 sweeps: the same from float32 rows into the
+// float32 QUARTERS image of k_interleave (element = 4 samples X(c, base + i +
+// m*Qs), m < 4), each pattern element the float sum of its group's fx
+// elements in channel order (x_c0 + x_c0+1 [+ x_c0+2 + x_c0+3]); the sweep
+// then adds pattern series instead of channels -- the reference's float64
+// channel sum regrouped, within the float32 parity bar (and exact for
+// integer-valued data).  Pads as k_interleave: value (per channel) / rotate.
+__global__ __launch_bounds__(256) void k_fx_patterns_xf(const float* __restrict__ x, InLayout lay,
+                                                        int64_t N, int64_t base, int64_t Qs,
+                                                        int64_t nR, int pad_mode,
+                                                        const float* __restrict__ padvals,
+                                                        const int4* __restrict__ pat,
+                                                        const int* __restrict__ gtab, int NG, int fx,
+                                                        float4* __restrict__ P) {
+  extern __shared__ __attribute__((aligned(16))) float4 Lf[];
+  const int g = blockIdx.x;
+  const int64_t j0 = (int64_t)blockIdx.y * kFxE;
+  const int p0 = gtab[g], p1 = gtab[g + 1];
+  const int lo = gtab[NG + 1 + 2 * g], hi = gtab[NG + 2 + 2 * g];
+  const int W = kFxE + hi - lo;
+  for (int k = 0; k < fx; ++k) {
+    const int c = g * fx + k;
+    const float pv = (pad_mode == PDD_PAD_VALUE) ? padvals[c] : 0.f;
+    for (int e = threadIdx.x; e < W; e += 256) {
+      const int64_t i = j0 + lo + e;
+      float v[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int64_t sm = base + i + m * Qs;
+        if (i < 0 || i >= nR) v[m] = 0.f;
+        else if (sm >= 0 && sm < N) v[m] = x[lay.at(c, sm)];
+        else if (pad_mode == PDD_PAD_ROTATE) v[m] = x[lay.at(c, wrap_mod(sm, N))];
+        else v[m] = pv;
+      }
+      Lf[k * W + e] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+  __syncthreads();
+  for (int p = p0; p < p1; ++p) {
+    const int4 q = pat[p];
+#pragma unroll
+    for (int e = threadIdx.x; e < kFxE; e += 256) {
+      const int64_t j = j0 + e;
+      if (j >= nR) break;
+      float4 s = Lf[e - lo];
+      const float4 b = Lf[W + e - lo + q.y];
+      s.x += b.x; s.y += b.y; s.z += b.z; s.w += b.w;
+      if (fx > 2) {
+        const float4 c = Lf[2 * W + e - lo + q.z], d = Lf[3 * W + e - lo + q.w];
+        s.x += c.x; s.y += c.y; s.z += c.z; s.w += c.w;
+        s.x += d.x; s.y += d.y; s.z += d.z; s.w += d.w;
+      }
+      P[(int64_t)p * nR + j] = s;
+    }
+  }
+}
+
 // n DMAs of 64 elements (1 KiB) each, q = first, first + step, ...
 __device__ __forceinline__ int stage_il_dma(uint32_t lds_dst, const float4* src, int ne, int first,
                                             int step, int lane) {
@@ -1006,7 +1063,6 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   constexpr int SLOT = il_slot(CC, DB);
   constexpr int MA = il_ma(NBUF), MR = il_mr(NBUF);
   constexpr int S = U16 ? 8 : 4;  // samples per 16-byte element (quarters / eighths)
-  static_assert(!FX || U16, "factorised sweeps run on the u16 eighths");
   static_assert(DPW == 4 && G == (U16 ? 2 : 4) && DPW * CC <= 64 && CC % 2 == 0,
                 "4 trials per wave, 4 (f32) or 2 (u16) groups; one lane per (channel, trial)");
   static_assert(NBUF >= 2 && MA >= 2 * NBUF - 2 && MR > MA, "ring geometry");
@@ -1532,6 +1588,9 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false, int fxs = 0)
 #endif
         default: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 3>;
       }
+    // float32 quarters (the channel sweep's f32 tiling)
+    if (v.S == 4 && v.NW == 14 && v.NLW == 2 && v.G == 4 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
+      return k_sweep_il<4, 4, 14, 2, 8, 2, false, true, 3>;
     return nullptr;
   }
 #define IL(NCW_, NLW_, CC_, NB_)                                                              \
@@ -1753,8 +1812,9 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
   if (p->fx) {
     // (ds > 1: the interleave pre-pass co-adds the raw rows into R and stage
     // 1 builds the patterns from R: sums of fx co-adds <= 4 * 1020 stay exact)
-    PDD_REQUIRE(u16 && p->dtype != PDD_F32 && !ex.r2_pad && !ex.R_pre && p->n_grp == 1,
-                "pdd_sweep_execute: factorised plans take single-group 8/16-bit input");
+    PDD_REQUIRE(u16 == (p->dtype != PDD_F32) && !ex.r2_pad && !ex.R_pre && p->n_grp == 1 &&
+                    (u16 || fx_direct),
+                "pdd_sweep_execute: factorised plans take single-group input (float32: raw rate)");
     P = static_cast<uint4*>(scratch(st, kScratchPattern, (size_t)((p->n_pat + 1) * nr_alloc) * sizeof(uint4)));
     if (!P) return -2;
   }
@@ -1818,7 +1878,11 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
       const dim3 gp((unsigned)NG, (unsigned)cdiv(nR, kFxE));
       const size_t lds_p = (size_t)(p->fx * (kFxE + p->fx_rspan)) * sizeof(uint4);
       const int64_t b0 = t_base + lo + x_off;
-      if (fx_direct && p->dtype == PDD_U8) {
+      if (fx_direct && p->dtype == PDD_F32) {
+        hipLaunchKernelGGL(k_fx_patterns_xf, gp, dim3(256), lds_p, st, (const float*)x, lay, N, b0,
+                           Qs, nR, pad_mode, padvals, (const int4*)p->d_pat, p->d_gtab, NG, p->fx,
+                           (float4*)P);
+      } else if (fx_direct && p->dtype == PDD_U8) {
         hipLaunchKernelGGL(k_fx_patterns_x<uint8_t>, gp, dim3(256), lds_p, st, (const uint8_t*)x, lay,
                            N, b0, Qs, nR, pad_mode, padvals, (const int4*)p->d_pat, p->d_gtab, NG,
                            p->fx, P);
@@ -1928,6 +1992,9 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
     while (g < NG) T.gtab[(size_t)(++g)] = (int)T.n_pat;
     if (!fits) T.gtab.clear();
   }
+  // float32 patterns are built only by the LDS stage 1 from the input rows
+  // (k_fx_patterns_xf: float adds)
+  if (v.S == 4 && T.gtab.empty()) return false;
   // (a quick screen: stage 1 + stage 2 adds against the channel sweep's)
   if (!force && (double)T.n_pat * fx + (double)D * NG > 0.75 * (double)D * C) return false;
   if (T.n_pat + 1 >= (1 << 20)) return false;
@@ -2049,12 +2116,20 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
     }
     for (const auto& ch : cw[(size_t)b])
       for (const auto& r : ch) el_f += (r[1] + 63) / 64 * 64;
-    cost_b += 1.15 * std::max(440.0 * (double)C, 1.15 * (double)el_b);
-    cost_f += 1.16 * std::max(110.0 * (double)C, 1.15 * (double)el_f);
+    if (v.S == 8) {
+      cost_b += 1.15 * std::max(440.0 * (double)C, 1.15 * (double)el_b);
+      cost_f += 1.16 * std::max(110.0 * (double)C, 1.15 * (double)el_f);
+    } else {
+      // float32 quarters (configs[1] f32: 1.18 M cycles per tile, compute-bound
+      // at ~1156 cycles per channel; staging alone ~1.28 cycles per element)
+      cost_b += std::max(1156.0 * (double)C, 1.28 * (double)el_b);
+      cost_f += std::max(1156.0 * (double)C / fx, 1.28 * (double)el_f);
+    }
   }
-  // stage 1 per time tile: every pattern's 2 KiB of eighths, written once
-  // for all trial blocks at ~6.7 B per CU cycle (k_fx_patterns_lds: 4.1 TB/s)
-  cost_f += (double)T.n_pat * 2048.0 / 6.7;
+  // stage 1 per time tile: every pattern's Tq elements (2 KiB of eighths, 4 KiB
+  // of quarters), written once for all trial blocks at ~6.7 B per CU cycle
+  // (k_fx_patterns_lds: 4.1 TB/s)
+  cost_f += (double)T.n_pat * (double)(Tq * 16) / 6.7;
   T.cost_b = cost_b;
   T.cost_f = cost_f;
   if (!force && cost_f > 0.9 * cost_b) return false;
@@ -2283,7 +2358,7 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
       FxTables T, T2;
       const bool force = (flags & PDD_SWEEP_FACTOR_FORCE) != 0;
       int fxg = 0;
-      if ((flags & PDD_SWEEP_FACTOR) && dtype != PDD_F32 && n_grp == 1 && v.S == 8 &&
+      if ((flags & PDD_SWEEP_FACTOR) && n_grp == 1 && v.S == (dtype == PDD_F32 ? 4 : 8) &&
           il_kernel_for(v, true)) {
         if (!(flags & PDD_SWEEP_FACTOR_G2) && fx_build(host_table, D, C, v, buf_e, 4, force, T))
           fxg = 4;
@@ -2312,7 +2387,7 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
         if (e == hipSuccess && !T.gtab.empty())
           e = hipMemcpy(p->d_gtab, T.gtab.data(), T.gtab.size() * sizeof(int), hipMemcpyHostToDevice);
         for (const void* kf : {(const void*)k_fx_patterns_lds, (const void*)k_fx_patterns_x<uint8_t>,
-                               (const void*)k_fx_patterns_x<uint16_t>})
+                               (const void*)k_fx_patterns_x<uint16_t>, (const void*)k_fx_patterns_xf})
           if (e == hipSuccess && !T.gtab.empty())
             e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)(4 * (kFxE + kFxRspan) * sizeof(uint4)));

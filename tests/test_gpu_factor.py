@@ -144,3 +144,63 @@ def test_factor_16bit_input_vs_oracle(gpu, input_max):
         plane = sw(torch.from_numpy(x).cuda()).cpu().numpy().astype(np.float64)
         np.testing.assert_array_equal(plane, want, err_msg="g %d" % g)
         sw.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pad", [0, 3.5, "mean", "rotate"])
+@pytest.mark.parametrize("descending", [True, False])
+@pytest.mark.parametrize("C,g", [(36, 4), (34, 2)])
+def test_factor_f32_small_grids_vs_oracle(gpu, pad, descending, C, g):
+    """Factorised FLOAT32 sweeps (k_fx_patterns_xf + k_sweep_il<..., FX> on the
+    float32 quarters): forced groups of 4 / 2, value / statistical / rotate
+    pads past the block edge, both band orders.  Integer-valued data with an
+    integer pad are bit-exact (every partial sum is an integer < 2^24);
+    fractional data and fractional pads within the float32 bar (1e-5 of the
+    row's max)."""
+    import torch
+    from conftest import rel_err
+    from pypulsar_amd.sweep import DMSweep
+    N, D = 6000, 64
+    freqs = band(C, descending=descending)
+    dms = np.linspace(0, 4.0, D)
+    tab = orc.sweep_table(dms, freqs, DT)
+    sw = DMSweep(dms, freqs, DT, dtype="f32", factor="force4" if g == 4 else "force2")
+    assert sw.factor_info(0)[0] == g
+    xi = u8_data(C, N, 51 + C).astype(np.float32)
+    xf = np.random.default_rng(52 + C).normal(3.0, 1.5, (C, N)).astype(np.float32)
+    for data, exact in ((xi, pad in (0, "rotate")), (xf, False)):
+        for trim in (True, False):
+            plane = sw(torch.from_numpy(data).cuda(), padval=pad, trim=trim).cpu().numpy()
+            want = orc.sweep_plane(data.astype(np.float64), tab, pad, n_out=plane.shape[1])
+            if exact:
+                np.testing.assert_array_equal(plane.astype(np.float64), want)
+            else:
+                assert rel_err(plane, want) <= 1e-5, (pad, trim, rel_err(plane, want))
+    sw.close()
+
+
+@pytest.mark.gpu
+def test_factor_f32_config1_geometry(gpu):
+    """BASELINE configs[1] geometry (1024 ch x 1024 DM, 0-1000 pc/cc, float32)
+    at N = 2^17, factorised over groups of 2 (forced): integer-valued data
+    equal the channel-by-channel f32 kernel bit for bit, fractional data the
+    oracle rows within 1e-5."""
+    import torch
+    from conftest import rel_err
+    from pypulsar_amd.sweep import DMSweep
+    C, N, D = 1024, 1 << 17, 1024
+    freqs = band(C)
+    dms = np.linspace(0, 1000, D)
+    fx = DMSweep(dms, freqs, DT, dtype="f32", factor="force2")
+    assert fx.factor_info(0)[0] == 2
+    plain = DMSweep(dms, freqs, DT, dtype="f32", factor=False)
+    xi = torch.from_numpy(u8_data(C, N, 43).astype(np.float32)).cuda()
+    assert torch.equal(fx(xi), plain(xi))
+    xf = np.random.default_rng(44).normal(0.0, 1.0, (C, N)).astype(np.float32)
+    a = fx(torch.from_numpy(xf).cuda())
+    rows = [0, 1, 511, 1023]
+    want = orc.sweep_plane(xf.astype(np.float64), orc.sweep_table(dms, freqs, DT)[rows], 0,
+                           n_out=a.shape[1])
+    assert rel_err(a[rows].cpu().numpy(), want) <= 1e-5
+    fx.close()
+    plain.close()
