@@ -2118,7 +2118,7 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
       for (const auto& r : ch) el_f += (r[1] + 63) / 64 * 64;
     if (v.S == 8) {
       cost_b += 1.15 * std::max(440.0 * (double)C, 1.15 * (double)el_b);
-      cost_f += 1.16 * std::max(110.0 * (double)C, 1.15 * (double)el_f);
+      cost_f += 1.07 * std::max(110.0 * (double)C, 1.15 * (double)el_f);
     } else {
       // float32 quarters (configs[1] f32: 1.18 M cycles per tile, compute-bound
       // at ~1156 cycles per channel; staging alone ~1.28 cycles per element)

@@ -162,7 +162,9 @@ def test_factor_f32_small_grids_vs_oracle(gpu, pad, descending, C, g):
     from pypulsar_amd.sweep import DMSweep
     N, D = 6000, 64
     freqs = band(C, descending=descending)
-    dms = np.linspace(0, 4.0, D)
+    # (DB = 56 trials per block: a narrower grid than the u16 tests' for
+    # groups of 4, whose pairs' pattern windows must fit one chunk buffer)
+    dms = np.linspace(0, 3.0 if g == 4 else 4.0, D)
     tab = orc.sweep_table(dms, freqs, DT)
     sw = DMSweep(dms, freqs, DT, dtype="f32", factor="force4" if g == 4 else "force2")
     assert sw.factor_info(0)[0] == g
