@@ -1155,11 +1155,22 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     // into its buffer at the per-channel offsets of the metadata rows
     // (loader 0 reads chunk k + MA's table entry one iteration ahead: a
     // scalar load's latency is not on the loaders' per-chunk path)
-    int e_next = (lw == 0 && MA < nchunk) ? cht_t[1 + MA] : 0;
+    // FXS bit 2 (factorised tiles): the metadata DMAs rotate over the
+    // loaders (chunk k's rows from loader k mod NLW), so loader 0 is not the
+    // one wave with ~5 more DMAs per chunk than the others; each loader reads
+    // its next chunk's table entry one turn (NLW chunks) ahead.
+    constexpr bool kRot = FX && (FXS & 4);
+    const int meta_first = kRot ? MA + ((lw - MA % NLW) % NLW + NLW) % NLW : MA;
+    int e_next = ((kRot || lw == 0) && meta_first < nchunk) ? cht_t[1 + meta_first] : 0;
     auto issue_meta = [&](int k) -> int {
-      if (lw != 0 || k >= nchunk) return 0;
+      if (k >= nchunk) return 0;
+      if (kRot ? (k % NLW != lw) : (lw != 0)) return 0;
       const int e = k < MA ? cht_t[1 + k] : e_next;
-      if (k >= MA && k + 1 < nchunk) e_next = cht_t[2 + k];
+      if (kRot) {
+        if (k >= MA && k + NLW < nchunk) e_next = cht_t[1 + k + NLW];
+      } else if (k >= MA && k + 1 < nchunk) {
+        e_next = cht_t[2 + k];
+      }
       const int n_int = (e >> 20) * ROW;
       int n = 0;
 #pragma unroll
@@ -1555,7 +1566,11 @@ static const Variant kU8Variants[] = {
                                         //   against 121.6, once the loaders read no LDS)
     {0, false, 4, 4, 4, 8, 8, 2, 2},    // f32 image of u8 data, DB 32
     {1, true, 8, 2, 1, 8, 1, 2, 0},     // generic u16, DB 8
-    {1, true, 8, 1, 1, 1, 1, 2, 0}};    // generic u16, DB 1
+    {1, true, 8, 1, 1, 1, 1, 2, 0}      // generic u16, DB 1
+#ifdef PDD_SWEEP_DEV
+    , {0, false, 8, 2, 4, 12, 8, 3, 4}  // dev (PDD_SWEEP_VARIANT=4): u16 eighths, 3 chunk buffers
+#endif
+};
 
 #ifdef PDD_SWEEP_DEV
 // experimental 8-bit MFMA tilings, tried first when PDD_SWEEP_MX=1
@@ -1585,9 +1600,15 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false, int fxs = 0)
         case 0: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 0>;
         case 1: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 1>;
         case 2: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 2>;
+        case 7: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 7>;
 #endif
         default: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 3>;
       }
+#ifdef PDD_SWEEP_DEV
+    if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 3)
+      return fxs == 7 ? k_sweep_il<2, 4, 12, 4, 8, 3, true, true, 7>
+                      : k_sweep_il<2, 4, 12, 4, 8, 3, true, true, 3>;
+#endif
     // float32 quarters (the channel sweep's f32 tiling)
     if (v.S == 4 && v.NW == 14 && v.NLW == 2 && v.G == 4 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
       return k_sweep_il<4, 4, 14, 2, 8, 2, false, true, 3>;
@@ -1599,6 +1620,9 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false, int fxs = 0)
     return k_sweep_il<4, 4, NCW_, NLW_, CC_, NB_>;
   if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.DPW == 4) {
     if (v.CC == 8 && v.NBUF == 2) return k_sweep_il<2, 4, 12, 4, 8, 2, true>;
+#ifdef PDD_SWEEP_DEV
+    if (v.CC == 8 && v.NBUF == 3) return k_sweep_il<2, 4, 12, 4, 8, 3, true>;
+#endif
   }
   IL(14, 2, 8, 2)
   IL(8, 2, 8, 2)

@@ -17,7 +17,9 @@ def band(C, lo=1250.0, hi=1550.0):
 kind = sys.argv[1] if len(sys.argv) > 1 else "f32"
 if kind == "f32":   # BASELINE configs[1]
     C, N, D, dt = 1024, 1 << 20, 1024, "f32"
-else:               # the configs[3] grid on a 2^20 block
+elif kind == "ns":  # the north-star grid on a 2^20 block (factorised, groups of 2)
+    C, N, D, dt = 4096, 1 << 20, 2048, "u8"
+else:               # the configs[3] grid on a 2^20 block (factorised, groups of 4)
     C, N, D, dt = 4096, 1 << 20, 4096, "u8"
 x = torch.randint(0, 256, (C, N), dtype=torch.uint8, device="cuda")
 if dt == "f32":
@@ -34,7 +36,7 @@ st = st[:blocks]
 comp = comp[:blocks]
 cw = st[comp]          # [n, 4]: 0, barrier, compute, 1
 lw = st[~comp]         # [n, 4]: vmcnt, barrier, issue, 0
-print(kind, info, "blocks", blocks)
+print(kind, info, "factor", sw.factor_info(1 if dt == "u8" else 0), "blocks", blocks)
 print("compute waves: barrier %.0f  compute %.0f  -> barrier share %.3f"
       % (cw[:, 1].mean(), cw[:, 2].mean(), cw[:, 1].sum() / (cw[:, 1].sum() + cw[:, 2].sum())))
 print("loader waves : vmcnt %.0f  barrier %.0f  issue %.0f"
