@@ -184,6 +184,8 @@ def test_plan_model_matches_kernel_tables():
     for name, model in (("kF32Variants", plan_model.F32), ("kU8Variants", plan_model.U8)):
         body = src[src.index("static const Variant %s[] = {" % name):]
         body = body[:body.index("};")]
+        # rows under #ifdef PDD_SWEEP_DEV are developer-build tilings only
+        body = re.sub(r"#ifdef PDD_SWEEP_DEV.*?#endif", "", body, flags=re.S)
         rows = [tuple(int(v) if v not in ("true", "false") else int(v == "true")
                       for v in (x.strip() for x in m.split(",")))
                 for m in re.findall(r"\{([-\w, ]+)\}", body)]
