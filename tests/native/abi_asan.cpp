@@ -61,7 +61,7 @@ static void sweep_case(std::mt19937& rng, int64_t C, int64_t N, int64_t D, int s
   if (rc != 0) return;
   int64_t n_pat = -1;
   const int fx = pdd_sweep_plan_factor(plan, &n_pat);
-  CHECK(fx == 0 || ((fx == 2 || fx == 4) && C % fx == 0 && n_pat > 0 && dtype != PDD_F32),
+  CHECK(fx == 0 || ((fx == 2 || fx == 4) && C % fx == 0 && n_pat > 0),
         "factor %d (%lld patterns) for C=%lld dtype=%d", fx, (long long)n_pat, (long long)C, dtype);
   if (fx) ++factorised_cases;
   int64_t info[8] = {0};
