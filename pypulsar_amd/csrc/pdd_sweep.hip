@@ -733,7 +733,7 @@ __global__ __launch_bounds__(256) void k_fx_patterns_lds(const uint4* __restrict
 // pattern of the group as k_fx_patterns_lds does.  Saves the image's write
 // and read, and the interleave launch, per segment (the per-rank work of a
 // DM-sharded step that does not shrink with the world size).
-template <typename InT>
+template <typename InT, bool NT = false>
 __global__ __launch_bounds__(256) void k_fx_patterns_x(const InT* __restrict__ x, InLayout lay,
                                                        int64_t N, int64_t base, int64_t Qs,
                                                        int64_t nR, int pad_mode,
@@ -747,9 +747,24 @@ __global__ __launch_bounds__(256) void k_fx_patterns_x(const InT* __restrict__ x
   const int p0 = gtab[g], p1 = gtab[g + 1];
   const int lo = gtab[NG + 1 + 2 * g], hi = gtab[NG + 2 + 2 * g];
   const int W = kFxE + hi - lo;
+  // a block whose rows lie inside [0, nR) and whose samples inside [0, N)
+  // (every block but the segment's edges) loads without per-sample tests
+  const int64_t s_lo = base + j0 + lo, s_hi = s_lo + W - 1 + 7 * Qs;
+  const bool inner = j0 + lo >= 0 && j0 + lo + W <= nR && s_lo >= 0 && s_hi < N;
   for (int k = 0; k < fx; ++k) {
     const int c = g * fx + k;
     const uint32_t pv = (pad_mode == PDD_PAD_VALUE) ? (uint32_t)padvals[c] : 0u;
+    if (inner) {
+      for (int e = threadIdx.x; e < W; e += 256) {
+        const int64_t sm = s_lo + e;
+        uint32_t v[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) v[m] = x[lay.at(c, sm + m * Qs)];
+        L[k * W + e] = make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16),
+                                  v[6] | (v[7] << 16));
+      }
+      continue;
+    }
     for (int e = threadIdx.x; e < W; e += 256) {
       const int64_t i = j0 + lo + e;
       uint32_t v[8];
@@ -775,8 +790,15 @@ __global__ __launch_bounds__(256) void k_fx_patterns_x(const InT* __restrict__ x
       const uint4 a = L[e - lo], b = L[W + e - lo + q.y];
       const uint4 c = fx > 2 ? L[2 * W + e - lo + q.z] : make_uint4(0u, 0u, 0u, 0u);
       const uint4 d = fx > 3 ? L[3 * W + e - lo + q.w] : make_uint4(0u, 0u, 0u, 0u);
-      P[(int64_t)p * nR + j] = make_uint4(a.x + b.x + c.x + d.x, a.y + b.y + c.y + d.y,
-                                          a.z + b.z + c.z + d.z, a.w + b.w + c.w + d.w);
+      if constexpr (NT) {
+        typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
+        const v4u_t r = {a.x + b.x + c.x + d.x, a.y + b.y + c.y + d.y, a.z + b.z + c.z + d.z,
+                         a.w + b.w + c.w + d.w};
+        __builtin_nontemporal_store(r, reinterpret_cast<v4u_t*>(P) + ((int64_t)p * nR + j));
+      } else {
+        P[(int64_t)p * nR + j] = make_uint4(a.x + b.x + c.x + d.x, a.y + b.y + c.y + d.y,
+                                            a.z + b.z + c.z + d.z, a.w + b.w + c.w + d.w);
+      }
     }
   }
 }
@@ -1341,6 +1363,8 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   static_assert(!U16 || DPW * CC <= 64, "one lane per (channel, trial) shift");
   typedef __attribute__((address_space(3))) u32x4_t lds_u32x4_t;
   uint64_t ts_poll = 0, ts_comp = 0, tA = 0, tB = 0;
+  constexpr bool kPreMeta = FX && (FXS & 8);
+  int vmeta_n = 0, ncc_n = 0;  // kPreMeta: the next chunk's shifts and count
   __builtin_amdgcn_s_barrier();  // prologue barrier (metadata landed)
   asm volatile("" ::: "memory");
   if (stamps) tB = __builtin_amdgcn_s_memtime();
@@ -1368,11 +1392,29 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     // last field is the chunk's channel count)
     typedef __attribute__((address_space(3))) int lds_int_t;
     const int ml = min(lane / DPW, CC - 1) * ROW + lane % DPW;
-    const int vmeta = *(const lds_int_t*)(uintptr_t)(meta_base + (uint32_t)((slot * SLOT + ml) * 4));
-    // (the channel count rides in a separate read: folding it into the shift
-    // read -- lanes >= DPW * CC -- measured 1.6% slower for u16, neutral for f32)
-    int ncc = __builtin_amdgcn_readfirstlane(*(const lds_int_t*)(uintptr_t)(
-        lds_addr_of(metar) + (uint32_t)((slot * SLOT + DB + 3) * 4))) >> 20;
+    auto read_shifts = [&](int sl) -> int {
+      return *(const lds_int_t*)(uintptr_t)(meta_base + (uint32_t)((sl * SLOT + ml) * 4));
+    };
+    auto read_count = [&](int sl) -> int {
+      return *(const lds_int_t*)(uintptr_t)(lds_addr_of(metar) + (uint32_t)((sl * SLOT + DB + 3) * 4));
+    };
+    int vmeta, ncc;
+    if constexpr (kPreMeta) {
+      // FXS bit 3: chunk k + 1's shifts and count are read during chunk k (its
+      // ring slot landed before barrier k), so no dependent LDS round trip
+      // stands between a barrier and the first sample read
+      vmeta = k == 0 ? read_shifts(slot) : vmeta_n;
+      ncc = __builtin_amdgcn_readfirstlane(k == 0 ? read_count(slot) : ncc_n) >> 20;
+      if (k + 1 < nchunk) {
+        vmeta_n = read_shifts((k + 1) % MR);
+        ncc_n = read_count((k + 1) % MR);
+      }
+    } else {
+      vmeta = read_shifts(slot);
+      // (the channel count rides in a separate read: folding it into the shift
+      // read -- lanes >= DPW * CC -- measured 1.6% slower for u16, neutral for f32)
+      ncc = __builtin_amdgcn_readfirstlane(read_count(slot)) >> 20;
+    }
 #ifdef PDD_SWEEP_DEV
     if (dbg & 64) ncc = cht_t[1 + k] >> 20;  // no barrier: the ring may not hold chunk k yet
 #endif
@@ -1601,6 +1643,7 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false, int fxs = 0)
         case 1: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 1>;
         case 2: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 2>;
         case 7: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 7>;
+        case 11: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 11>;
 #endif
         default: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 3>;
       }
@@ -1902,7 +1945,16 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
       const dim3 gp((unsigned)NG, (unsigned)cdiv(nR, kFxE));
       const size_t lds_p = (size_t)(p->fx * (kFxE + p->fx_rspan)) * sizeof(uint4);
       const int64_t b0 = t_base + lo + x_off;
-      if (fx_direct && p->dtype == PDD_F32) {
+#ifdef PDD_SWEEP_DEV
+      static const bool s1_nt = getenv("PDD_FX_S1_NT") && atoi(getenv("PDD_FX_S1_NT"));
+#else
+      constexpr bool s1_nt = false;
+#endif
+      if (fx_direct && p->dtype == PDD_U8 && s1_nt) {
+        hipLaunchKernelGGL((k_fx_patterns_x<uint8_t, true>), gp, dim3(256), lds_p, st, (const uint8_t*)x,
+                           lay, N, b0, Qs, nR, pad_mode, padvals, (const int4*)p->d_pat, p->d_gtab, NG,
+                           p->fx, P);
+      } else if (fx_direct && p->dtype == PDD_F32) {
         hipLaunchKernelGGL(k_fx_patterns_xf, gp, dim3(256), lds_p, st, (const float*)x, lay, N, b0,
                            Qs, nR, pad_mode, padvals, (const int4*)p->d_pat, p->d_gtab, NG, p->fx,
                            (float4*)P);
@@ -2411,7 +2463,8 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
         if (e == hipSuccess && !T.gtab.empty())
           e = hipMemcpy(p->d_gtab, T.gtab.data(), T.gtab.size() * sizeof(int), hipMemcpyHostToDevice);
         for (const void* kf : {(const void*)k_fx_patterns_lds, (const void*)k_fx_patterns_x<uint8_t>,
-                               (const void*)k_fx_patterns_x<uint16_t>, (const void*)k_fx_patterns_xf})
+                               (const void*)k_fx_patterns_x<uint16_t>, (const void*)k_fx_patterns_xf,
+                               (const void*)k_fx_patterns_x<uint8_t, true>})
           if (e == hipSuccess && !T.gtab.empty())
             e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)(4 * (kFxE + kFxRspan) * sizeof(uint4)));

@@ -12,7 +12,7 @@ for run in ${RUNS:-"config3:4:1" "config3:4:2" "northstar:2:0" "northstar:2:2" "
   PDD_SWEEP_VARIANT=${var:-0} PDD_FX_STAGE=$st timeout -k 10 200 python bench.py --config $c --factor $g --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > $O/b.json 2> $O/b.err || { echo "FAIL $run"; tail -3 $O/b.err; exit 1; }
   echo "$c g=$g stage=$st variant=${var:-0}: $(k $O/b.json)"
 done
-for st in ${RUNT:-2}; do
+for st in ${RUNT-2}; do
   PDD_SWEEP_VARIANT=${RUNV:-0} PDD_FX_STAGE=$st timeout -k 10 600 python -u -m pytest -m gpu -x -q --timeout 200 --timeout-method thread ${TF:-tests} -k "${TK:-factor or config or sweep}" > $O/pytest_$st.log 2>&1
   rc=$?; echo "tests stage=$st: $(tail -1 $O/pytest_$st.log)"; [ $rc -eq 0 ] || exit $rc
 done
