@@ -177,13 +177,17 @@ typedef struct pdd_sweep_plan pdd_sweep_plan;
 int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int dtype,
                           pdd_sweep_plan** plan);
 /* The same with plan flags (pdd_sweep_plan_create = PDD_SWEEP_FACTOR):
- * PDD_SWEEP_FACTOR lets an integer plan (PDD_U8 / PDD_U16, single group)
- * sweep EXACTLY factorised over groups of 4 (or 2) adjacent channels when
- * that pays: each
+ * PDD_SWEEP_FACTOR lets a single-group plan sweep factorised over groups of
+ * 4 (or 2) adjacent channels when the plan's cost model says it pays: each
  * group's distinct relative-shift patterns are summed once (stage 1), and
- * every trial adds its pattern series at the group's base shift (stage 2) --
- * the same integer samples as the channel-by-channel sum, so the plane is
- * bit-identical; flags 0 forces the channel-by-channel kernel. */
+ * every trial adds its pattern series at the group's base shift (stage 2).
+ * Integer plans (PDD_U8 / PDD_U16, also through pdd_sweep_execute_ds) sum
+ * the same integer samples as the channel-by-channel kernel: the plane is
+ * bit-identical.  PDD_F32 plans regroup the float32 channel sum (within the
+ * float32 bar; exact for integer-valued data).  Flags 0 forces the
+ * channel-by-channel kernel.  Factorised plans take the plain and the
+ * pieces layouts and column offsets; they do not chain
+ * (pdd_subband_chain). */
 #define PDD_SWEEP_FACTOR 1
 /* with PDD_SWEEP_FACTOR: factorise whenever the windows fit, paying or not
  * (tests of small grids) */
