@@ -938,16 +938,19 @@ __device__ __forceinline__ int stage_il_dma_s(uint32_t lds_dst, const float4* sr
       continue;
     }
     switch ((PDD_DMA_MODES && (mode & 1024)) ? 1 : min(4, nq - q)) {  // (1024, timing only: a run's first DMA)
-      case 1: PDD_DMA_S("global_load_lds_dwordx4 %1, %2\n\t"); break;
-      case 2: PDD_DMA_S("global_load_lds_dwordx4 %1, %2\n\t"
-                        "global_load_lds_dwordx4 %1, %2 offset:1024\n\t"); break;
-      case 3: PDD_DMA_S("global_load_lds_dwordx4 %1, %2\n\t"
-                        "global_load_lds_dwordx4 %1, %2 offset:1024\n\t"
-                        "global_load_lds_dwordx4 %1, %2 offset:2048\n\t"); break;
-      default: PDD_DMA_S("global_load_lds_dwordx4 %1, %2\n\t"
-                         "global_load_lds_dwordx4 %1, %2 offset:1024\n\t"
-                         "global_load_lds_dwordx4 %1, %2 offset:2048\n\t"
-                         "global_load_lds_dwordx4 %1, %2 offset:3072\n\t"); break;
+#ifndef PDD_DMA_POL
+#define PDD_DMA_POL ""  // dev builds: -DPDD_DMA_POL='" nt"' (cache-policy probes)
+#endif
+      case 1: PDD_DMA_S("global_load_lds_dwordx4 %1, %2" PDD_DMA_POL "\n\t"); break;
+      case 2: PDD_DMA_S("global_load_lds_dwordx4 %1, %2" PDD_DMA_POL "\n\t"
+                        "global_load_lds_dwordx4 %1, %2 offset:1024" PDD_DMA_POL "\n\t"); break;
+      case 3: PDD_DMA_S("global_load_lds_dwordx4 %1, %2" PDD_DMA_POL "\n\t"
+                        "global_load_lds_dwordx4 %1, %2 offset:1024" PDD_DMA_POL "\n\t"
+                        "global_load_lds_dwordx4 %1, %2 offset:2048" PDD_DMA_POL "\n\t"); break;
+      default: PDD_DMA_S("global_load_lds_dwordx4 %1, %2" PDD_DMA_POL "\n\t"
+                         "global_load_lds_dwordx4 %1, %2 offset:1024" PDD_DMA_POL "\n\t"
+                         "global_load_lds_dwordx4 %1, %2 offset:2048" PDD_DMA_POL "\n\t"
+                         "global_load_lds_dwordx4 %1, %2 offset:3072" PDD_DMA_POL "\n\t"); break;
 #undef PDD_DMA_S
     }
   }
@@ -1643,9 +1646,9 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false, int fxs = 0)
         case 1: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 1>;
         case 2: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 2>;
         case 7: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 7>;
-        case 11: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 11>;
+        case 3: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 3>;
 #endif
-        default: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 3>;
+        default: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 11>;
       }
 #ifdef PDD_SWEEP_DEV
     if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 3)
@@ -1724,13 +1727,15 @@ static int debug_flags() {
 // window records loaded two chunks ahead (their load latency off the
 // per-chunk barrier path).  Round 4 (dev builds, same box, kernel ms per
 // launch; configs[3] g 4 / north star g 2): 1: 74.0 / 106.9 (round 3), 0:
-// - / 100.8, 2: 86.8 / 111.1, 3: 68.0 / 97.6 -> 3 for both group sizes.
+// - / 100.8, 2: 86.8 / 111.1, 3: 68.0 / 97.6.  Bit 3 (compute waves read the
+// next chunk's shifts and count during the current chunk): 3 -> 11: 68.4 ->
+// 67.5 / 99.7 -> 98.8 -> 11 for both group sizes.
 static int fx_stage_for(int g) {
   (void)g;
 #ifdef PDD_SWEEP_DEV
   if (const char* e = getenv("PDD_FX_STAGE")) return atoi(e);
 #endif
-  return 3;
+  return 11;
 }
 static int forced_variant() {
 #ifdef PDD_SWEEP_DEV
