@@ -993,15 +993,23 @@ __host__ __device__ constexpr int il_meta_bytes(int nbuf, int cc, int db) {
 // group re-reads each staged element ~GT*GJ*(Tq+S)/(GT*Tq + GJ*S) times from
 // L2.  Leftover time tiles (n_tblk % 8) follow in natural order.
 // dbg bit 4: plain XCD-contiguous order (trial block fastest); bit 5: natural.
-__device__ __forceinline__ void il_tile_of(int bid, int n_tblk, int n_dblk, int dbg, int& dblk,
-                                           int& tblk) {
 #ifndef PDD_IL_GT
 #define PDD_IL_GT 8
 #endif
 #ifndef PDD_IL_GJ
 #define PDD_IL_GJ 4
 #endif
-  constexpr int GT = PDD_IL_GT, GJ = PDD_IL_GJ;
+// factorised tiles (their own tile-order shape: trial blocks of one time tile
+// share pattern rows, so the shapes are measured separately)
+#ifndef PDD_FX_GT
+#define PDD_FX_GT PDD_IL_GT
+#endif
+#ifndef PDD_FX_GJ
+#define PDD_FX_GJ PDD_IL_GJ
+#endif
+template <int GT = PDD_IL_GT, int GJ = PDD_IL_GJ>
+__device__ __forceinline__ void il_tile_of(int bid, int n_tblk, int n_dblk, int dbg, int& dblk,
+                                           int& tblk) {
   const int total = n_tblk * n_dblk;
   if (dbg & 32) {
     dblk = bid % n_dblk;
@@ -1107,7 +1115,8 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
 #define IL_TILE_SETUP                                                         \
   int dblk, tblk;                                                             \
   const int grp = tile / per_grp;                                             \
-  il_tile_of(tile - grp * per_grp, n_tblk, n_dblk, dbg, dblk, tblk);          \
+  il_tile_of<FX ? PDD_FX_GT : PDD_IL_GT, FX ? PDD_FX_GJ : PDD_IL_GJ>(           \
+      tile - grp * per_grp, n_tblk, n_dblk, dbg, dblk, tblk);                 \
   if (PDD_DMA_MODES && (dbg & 384)) tblk = (dbg & 128) ? 0 : (tblk & 7);          \
   const float4* R = R0 + (int64_t)grp * C * nR;                               \
   const int64_t t0 = (int64_t)tblk * Tq;                                      \
