@@ -926,6 +926,9 @@ __device__ __forceinline__ int stage_il_dma_win(uint32_t lds_dst, const float4* 
 // VALU address arithmetic.  `nq` pieces of 64 elements.
 __device__ __forceinline__ int stage_il_dma_s(uint32_t lds_dst, const float4* src, int nq,
                                               uint32_t voff, int mode = 0) {
+  // (timing only, 2048: a window's last piece is not staged -- what the
+  // staged bytes cost, not what they are)
+  if (PDD_DMA_MODES && (mode & 2048) && nq > 1) --nq;
   for (int q = 0; q < nq; q += 4) {
     const float4* s = src + q * 64;
     const uint32_t m = __builtin_amdgcn_readfirstlane(lds_dst + q * 1024);
@@ -1157,7 +1160,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
         const uint32_t hi32 = __builtin_amdgcn_readlane((uint32_t)(sv >> 32), i);
         n += stage_il_dma_s(__builtin_amdgcn_readlane(dv, i),
                             (const float4*)(((uint64_t)hi32 << 32) | lo32),
-                            __builtin_amdgcn_readlane(qv, i), voff16, dbg & 1536);
+                            __builtin_amdgcn_readlane(qv, i), voff16, dbg & 3584);
       }
       return n;
     }
