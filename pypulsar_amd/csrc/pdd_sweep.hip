@@ -1149,70 +1149,6 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const int b = k % NBUF;
     const int nw = __builtin_amdgcn_readlane(rec.w, 0) >> 20;
     int n = 0;
-    if constexpr ((FXS & 16) != 0) {
-      // Packed chunk (FXS bit 4): the windows lie back to back in the buffer,
-      // so the chunk is ceil(total / 64) pieces of 64 elements, split into
-      // contiguous ranges over the loaders; a piece that straddles two
-      // windows takes each lane's source from its own window (per-lane
-      // addresses).  Lane i = window i: vb = the address buffer element e
-      // would have if window i held it (source - offset), so element e of
-      // window i comes from vb_i + 16 e.
-      const int nw = __builtin_amdgcn_readlane(rec.w, 0) >> 20;
-      const bool act = lane < nw;
-      const int endv = act ? rec.z + (rec.y & 0xffff) : 0x7fffffff;
-      const uint64_t vb = (uint64_t)(R + (int64_t)(rec.w & 0xfffff) * nR + (t0 + rec.x - lo)) -
-                          (uint64_t)(uint32_t)rec.z * 16u;
-      const int total = __builtin_amdgcn_readlane(endv, nw - 1);
-      const int P = (total + 63) >> 6;
-      const int p_hi = (P * (first + 1)) / step;
-      const uint32_t m_base = img_lds + (uint32_t)(b * buf_e * 16);
-      int n = 0;
-      for (int p = (P * first) / step; p < p_hi;) {
-        const int e0 = p * 64;
-        const int a = __popcll(__ballot(act && endv <= e0));
-        const int endA = __builtin_amdgcn_readlane(endv, a);
-        const uint32_t alo = __builtin_amdgcn_readlane((uint32_t)vb, a);
-        const uint32_t ahi = __builtin_amdgcn_readlane((uint32_t)(vb >> 32), a);
-        const uint32_t m = m_base + (uint32_t)e0 * 16u;
-        const uint64_t va = (((uint64_t)ahi << 32) | alo) + (uint64_t)(uint32_t)(e0 + lane) * 16u;
-        uint32_t keep;
-        const int run = min(4, p_hi - p);
-        if (e0 + 64 * run <= endA) {
-          // `run` pieces inside window a: one address, instruction offsets
-#define PDD_DMA_V(TEXT)                                                                        \
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t" TEXT "s_mov_b32 m0, %0" \
-               : "=&s"(keep) : "v"(va), "s"(m) : "memory")
-          switch (run) {
-            case 1: PDD_DMA_V("global_load_lds_dwordx4 %1, off\n\t"); break;
-            case 2: PDD_DMA_V("global_load_lds_dwordx4 %1, off\n\t"
-                              "global_load_lds_dwordx4 %1, off offset:1024\n\t"); break;
-            case 3: PDD_DMA_V("global_load_lds_dwordx4 %1, off\n\t"
-                              "global_load_lds_dwordx4 %1, off offset:1024\n\t"
-                              "global_load_lds_dwordx4 %1, off offset:2048\n\t"); break;
-            default: PDD_DMA_V("global_load_lds_dwordx4 %1, off\n\t"
-                               "global_load_lds_dwordx4 %1, off offset:1024\n\t"
-                               "global_load_lds_dwordx4 %1, off offset:2048\n\t"
-                               "global_load_lds_dwordx4 %1, off offset:3072\n\t"); break;
-          }
-          n += run;
-          p += run;
-        } else {
-          // one piece, possibly straddling windows a and a + 1
-          const int bi = min(a + 1, nw - 1);
-          const uint32_t blo = __builtin_amdgcn_readlane((uint32_t)vb, bi);
-          const uint32_t bhi = __builtin_amdgcn_readlane((uint32_t)(vb >> 32), bi);
-          const uint64_t vbb = (((uint64_t)bhi << 32) | blo) + (uint64_t)(uint32_t)(e0 + lane) * 16u;
-          const uint64_t vaa = e0 + lane >= endA ? vbb : va;
-          asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                       "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                       : "=&s"(keep) : "v"(vaa), "s"(m) : "memory");
-          ++n;
-          ++p;
-        }
-#undef PDD_DMA_V
-      }
-      return n;
-    }
     if constexpr (FXS & 1) {
       // lane i = window i: its source, LDS address and piece count in one
       // pass, then this loader's windows (i = first mod step) from SGPRs
@@ -1723,7 +1659,6 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false, int fxs = 0)
         case 2: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 2>;
         case 7: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 7>;
         case 3: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 3>;
-        case 27: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 27>;
 #endif
         default: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 11>;
       }
@@ -2098,7 +2033,7 @@ struct FxTables {
   double cost_b = 0, cost_f = 0;   // modelled cycles per time tile: channel sweep / factorised
 };
 static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v, int64_t buf_e,
-                     int fx, bool force, FxTables& T, bool packed = false) {
+                     int fx, bool force, FxTables& T) {
   if (C % fx != 0 || C < 2 * fx) return false;
   const int64_t NG = C / fx, DB = v.DB(), ROW = DB + 4, Tq = 64 * v.G;
   const int64_t n_dblk = cdiv(D, DB);
@@ -2164,13 +2099,7 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
   std::vector<std::vector<int>> rows_of((size_t)n_dblk);  // per block: mt rows [row][ROW]
   std::vector<std::vector<int>> chunks((size_t)n_dblk);
   std::vector<std::vector<std::vector<std::array<int, 4>>>> cw((size_t)n_dblk);
-  // window footprint in a chunk buffer: 64-element granules, or (packed
-  // chunks, FXS bit 4) back to back with 64 elements of slack per chunk for
-  // the last piece
-  auto gran = [&](int span) -> int64_t {
-    return packed ? (int64_t)(Tq + span) : (Tq + span + 63) / 64 * 64;
-  };
-  const int64_t slack = packed ? 64 : 0;
+  auto gran = [&](int span) -> int64_t { return (Tq + span + 63) / 64 * 64; };
   int64_t rows_pb = 0;
   double cost_b = 0, cost_f = 0;
   for (int64_t b = 0; b < n_dblk; ++b) {
@@ -2243,9 +2172,8 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
                           const std::vector<std::array<int, 3>>& wb) -> bool {
       const int64_t need = need_of(wa) + need_of(wb);
       const int64_t nwin = (int64_t)(wa.size() + wb.size());
-      if (need + slack > buf_e || nwin > kFxWin) return false;
-      if (nrow + 2 > v.CC || used + need + slack > buf_e || (int64_t)rec.size() + nwin > kFxWin)
-        close();
+      if (need > buf_e || nwin > kFxWin) return false;
+      if (nrow + 2 > v.CC || used + need > buf_e || (int64_t)rec.size() + nwin > kFxWin) close();
       place(ga, wa);
       place(gb, wb);
       return true;
@@ -2525,11 +2453,9 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
       int fxg = 0;
       if ((flags & PDD_SWEEP_FACTOR) && n_grp == 1 && v.S == (dtype == PDD_F32 ? 4 : 8) &&
           il_kernel_for(v, true)) {
-        const bool packed = (fx_stage_for(0) & 16) != 0;
-        if (!(flags & PDD_SWEEP_FACTOR_G2) && fx_build(host_table, D, C, v, buf_e, 4, force, T, packed))
+        if (!(flags & PDD_SWEEP_FACTOR_G2) && fx_build(host_table, D, C, v, buf_e, 4, force, T))
           fxg = 4;
-        if (!(flags & PDD_SWEEP_FACTOR_G4) &&
-            fx_build(host_table, D, C, v, buf_e, 2, force, T2, packed) &&
+        if (!(flags & PDD_SWEEP_FACTOR_G4) && fx_build(host_table, D, C, v, buf_e, 2, force, T2) &&
             (fxg == 0 || T2.cost_f < T.cost_f)) {
           fxg = 2;
           std::swap(T, T2);
