@@ -960,6 +960,41 @@ __device__ __forceinline__ int stage_il_dma_s(uint32_t lds_dst, const float4* sr
   return nq;
 }
 
+// The same for a window of nq pieces as ONE asm block per run of up to four:
+// M0 set once, then the pieces with instruction offsets, each after the
+// first behind an s_cmp / s_cbranch on the remaining count (the compiler's
+// switch over min(4, nq - q) above became a tree of ~20 scalar instructions
+// and four branches per run).  Returns the DMAs issued.
+__device__ __forceinline__ int stage_il_dma_s2(uint32_t lds_dst, const float4* src, int nq,
+                                               uint32_t voff) {
+  for (int q = 0; q < nq; q += 4) {
+    const float4* s = src + q * 64;
+    const uint32_t m = __builtin_amdgcn_readfirstlane(lds_dst + q * 1024);
+    const int left = __builtin_amdgcn_readfirstlane(nq - q);
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2\n\t"
+        "s_cmp_lt_i32 %4, 2\n\t"
+        "s_cbranch_scc1 1f\n\t"
+        "global_load_lds_dwordx4 %1, %2 offset:1024\n\t"
+        "s_cmp_lt_i32 %4, 3\n\t"
+        "s_cbranch_scc1 1f\n\t"
+        "global_load_lds_dwordx4 %1, %2 offset:2048\n\t"
+        "s_cmp_lt_i32 %4, 4\n\t"
+        "s_cbranch_scc1 1f\n\t"
+        "global_load_lds_dwordx4 %1, %2 offset:3072\n"
+        "1:\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(s), "s"(m), "s"(left)
+        : "memory", "scc");
+  }
+  return nq;
+}
+
 // Synchronisation of k_sweep_il: one s_barrier per chunk.  Before barrier k
 // the loader waves retire chunk k's DMAs with a counted vmcnt (chunks k+1 ..
 // k+NBUF-2 stay in flight); after it they refill the buffer chunk k-1 used.
@@ -1158,9 +1193,14 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       for (int i = first; i < nw; i += step) {
         const uint32_t lo32 = __builtin_amdgcn_readlane((uint32_t)sv, i);
         const uint32_t hi32 = __builtin_amdgcn_readlane((uint32_t)(sv >> 32), i);
-        n += stage_il_dma_s(__builtin_amdgcn_readlane(dv, i),
-                            (const float4*)(((uint64_t)hi32 << 32) | lo32),
-                            __builtin_amdgcn_readlane(qv, i), voff16, dbg & 3584);
+        if constexpr ((FXS & 32) != 0)
+          n += stage_il_dma_s2(__builtin_amdgcn_readlane(dv, i),
+                               (const float4*)(((uint64_t)hi32 << 32) | lo32),
+                               __builtin_amdgcn_readlane(qv, i), voff16);
+        else
+          n += stage_il_dma_s(__builtin_amdgcn_readlane(dv, i),
+                              (const float4*)(((uint64_t)hi32 << 32) | lo32),
+                              __builtin_amdgcn_readlane(qv, i), voff16, dbg & 3584);
       }
       return n;
     }
@@ -1626,6 +1666,8 @@ static const Variant kU8Variants[] = {
     {1, true, 8, 1, 1, 1, 1, 2, 0}      // generic u16, DB 1
 #ifdef PDD_SWEEP_DEV
     , {0, false, 8, 2, 4, 12, 8, 3, 4}  // dev (PDD_SWEEP_VARIANT=4): u16 eighths, 3 chunk buffers
+    , {0, false, 8, 2, 4, 10, 8, 2, 6}  // dev (5): 10 compute + 6 loader waves, DB 40
+    , {0, false, 8, 2, 4, 8, 8, 2, 8}   // dev (6): 8 compute + 8 loader waves, DB 32
 #endif
 };
 
@@ -1659,10 +1701,15 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false, int fxs = 0)
         case 2: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 2>;
         case 7: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 7>;
         case 3: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 3>;
+        case 43: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 43>;
 #endif
         default: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 11>;
       }
 #ifdef PDD_SWEEP_DEV
+    if (v.S == 8 && v.NW == 10 && v.NLW == 6 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
+      return k_sweep_il<2, 4, 10, 6, 8, 2, true, true, 11>;
+    if (v.S == 8 && v.NW == 8 && v.NLW == 8 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
+      return k_sweep_il<2, 4, 8, 8, 8, 2, true, true, 11>;
     if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 3)
       return fxs == 7 ? k_sweep_il<2, 4, 12, 4, 8, 3, true, true, 7>
                       : k_sweep_il<2, 4, 12, 4, 8, 3, true, true, 3>;
@@ -1680,6 +1727,10 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false, int fxs = 0)
     if (v.CC == 8 && v.NBUF == 2) return k_sweep_il<2, 4, 12, 4, 8, 2, true>;
 #ifdef PDD_SWEEP_DEV
     if (v.CC == 8 && v.NBUF == 3) return k_sweep_il<2, 4, 12, 4, 8, 3, true>;
+  }
+  if (v.S == 8 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2) {
+    if (v.NW == 10 && v.NLW == 6) return k_sweep_il<2, 4, 10, 6, 8, 2, true>;
+    if (v.NW == 8 && v.NLW == 8) return k_sweep_il<2, 4, 8, 8, 8, 2, true>;
 #endif
   }
   IL(14, 2, 8, 2)
