@@ -1270,11 +1270,11 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
         // the record of chunk k was loaded an iteration ahead (the wait for
         // it is the one this iteration already did); load chunk k + 1's now
         const int4 rec = rec_next;
-        int n = fx_issue(k, rec, lw, NLW);
         if constexpr ((FXS & 2) != 0) {
           rec_next = rec_next2;  // (chunk k + 2's record: rec_ahead, after the metadata)
-          return n;
+          return fx_issue(k, rec, lw, NLW);
         }
+        int n = fx_issue(k, rec, lw, NLW);
         if (k + 1 < nchunk) {
           rec_next = fx_rec(k + 1);
           ++n;  // rides on the counted vmcnt

@@ -7,7 +7,7 @@ O=gpurun_out/fxs; mkdir -p $O
 k() { python -c "
 import json,sys;d=json.load(open(sys.argv[1]));r=d['roofline']
 print('kernel %.2f ms  step %.1f ms  value %.3e' % (r['kernel_ms_per_launch'], d['ms_per_step'], d['value']))" $1; }
-for run in ${RUNS:-"config3:4:1" "config3:4:2" "northstar:2:0" "northstar:2:2" "northstar:4:2"}; do
+for run in ${RUNS-"config3:4:1" "config3:4:2" "northstar:2:0" "northstar:2:2" "northstar:4:2"}; do
   IFS=: read c g st var <<< "$run"
   PDD_SWEEP_VARIANT=${var:-0} PDD_FX_STAGE=$st timeout -k 10 200 python bench.py --config $c --factor $g --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > $O/b.json 2> $O/b.err || { echo "FAIL $run"; tail -3 $O/b.err; exit 1; }
   echo "$c g=$g stage=$st variant=${var:-0}: $(k $O/b.json)"
