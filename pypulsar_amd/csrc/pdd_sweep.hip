@@ -1701,9 +1701,9 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false, int fxs = 0)
         case 2: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 2>;
         case 7: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 7>;
         case 3: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 3>;
-        case 43: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 43>;
+        case 11: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 11>;
 #endif
-        default: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 11>;
+        default: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 43>;
       }
 #ifdef PDD_SWEEP_DEV
     if (v.S == 8 && v.NW == 10 && v.NLW == 6 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
@@ -1716,7 +1716,7 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false, int fxs = 0)
 #endif
     // float32 quarters (the channel sweep's f32 tiling)
     if (v.S == 4 && v.NW == 14 && v.NLW == 2 && v.G == 4 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
-      return k_sweep_il<4, 4, 14, 2, 8, 2, false, true, 3>;
+      return k_sweep_il<4, 4, 14, 2, 8, 2, false, true, 43>;
     return nullptr;
   }
 #define IL(NCW_, NLW_, CC_, NB_)                                                              \
@@ -1792,13 +1792,16 @@ static int debug_flags() {
 // launch; configs[3] g 4 / north star g 2): 1: 74.0 / 106.9 (round 3), 0:
 // - / 100.8, 2: 86.8 / 111.1, 3: 68.0 / 97.6.  Bit 3 (compute waves read the
 // next chunk's shifts and count during the current chunk): 3 -> 11: 68.4 ->
-// 67.5 / 99.7 -> 98.8 -> 11 for both group sizes.
+// 67.5 / 99.7 -> 98.8.  Bit 5 (a window's DMA runs as one asm block with
+// the piece count tested inside it; the compiler's switch was a tree of ~20
+// scalar instructions and four branches per run): 11 -> 43: 67.2 -> 64.7 /
+// 97.5 -> 94.2 -> 43 for both group sizes.
 static int fx_stage_for(int g) {
   (void)g;
 #ifdef PDD_SWEEP_DEV
   if (const char* e = getenv("PDD_FX_STAGE")) return atoi(e);
 #endif
-  return 11;
+  return 43;
 }
 static int forced_variant() {
 #ifdef PDD_SWEEP_DEV
