@@ -1879,7 +1879,10 @@ static int64_t il_seg_samples(const pdd_sweep_plan* p, hipStream_t st) {
   int64_t budget = (int64_t)16 << 30;
   // factorised plans also hold the stage-1 pattern image (n_pat + 1 rows)
   const int64_t rows = C + (p->fx ? p->n_pat + 2 : 0);
-  if (p->fx) budget = (int64_t)40 << 30;
+  // (80 GiB: configs[3] in 4 launches of 1.04 M columns -- 572.9 against 578.3
+  // ms per step with 8 launches of 40 GiB; the free-memory cap below keeps
+  // smaller or busier GPUs on more, shorter segments)
+  if (p->fx) budget = (int64_t)80 << 30;
   if (const char* e = getenv("PDD_SWEEP_SEG_BYTES")) {
     budget = std::max<int64_t>(atoll(e), 1 << 16);
   } else {
