@@ -823,9 +823,20 @@ __global__ __launch_bounds__(256) void k_fx_patterns_xf(const float* __restrict_
   const int p0 = gtab[g], p1 = gtab[g + 1];
   const int lo = gtab[NG + 1 + 2 * g], hi = gtab[NG + 2 + 2 * g];
   const int W = kFxE + hi - lo;
+  // interior blocks load without per-sample tests (as k_fx_patterns_x)
+  const int64_t s_lo = base + j0 + lo, s_hi = s_lo + W - 1 + 3 * Qs;
+  const bool inner = j0 + lo >= 0 && j0 + lo + W <= nR && s_lo >= 0 && s_hi < N;
   for (int k = 0; k < fx; ++k) {
     const int c = g * fx + k;
     const float pv = (pad_mode == PDD_PAD_VALUE) ? padvals[c] : 0.f;
+    if (inner) {
+      for (int e = threadIdx.x; e < W; e += 256) {
+        const int64_t sm = s_lo + e;
+        Lf[k * W + e] = make_float4(x[lay.at(c, sm)], x[lay.at(c, sm + Qs)], x[lay.at(c, sm + 2 * Qs)],
+                                    x[lay.at(c, sm + 3 * Qs)]);
+      }
+      continue;
+    }
     for (int e = threadIdx.x; e < W; e += 256) {
       const int64_t i = j0 + lo + e;
       float v[4];
@@ -2280,6 +2291,10 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
   // of quarters), written once for all trial blocks at ~6.7 B per CU cycle
   // (k_fx_patterns_lds: 4.1 TB/s)
   cost_f += (double)T.n_pat * (double)(Tq * 16) / 6.7;
+  // the channel sweep's interleave pre-pass: every channel's Tq elements per
+  // time tile, written and read once (factorised plans build their pattern
+  // rows from the input directly)
+  cost_b += (double)C * (double)(Tq * 16) * 2.0 / 6.7;
   T.cost_b = cost_b;
   T.cost_f = cost_f;
   if (!force && cost_f > 0.9 * cost_b) return false;
