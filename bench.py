@@ -569,8 +569,12 @@ def sweep_bench(args, cfg, rank, world, dev):
                        "parallelism": "%s%d" % ({"timeblock": "tb", "timeshard": "ts"}
                                                 .get(mode, "dm"), world),
                        "rccl_world_size": rccl_world, "plan": plan,
-                       "method": ("exact factorisation over groups of %d channels (%d pattern "
-                                  "series; plane bit-identical to the channel-by-channel sum)"
+                       "method": (("exact factorisation over groups of %d channels (%d pattern "
+                                   "series; plane bit-identical to the channel-by-channel sum)"
+                                   if dtype == "u8" else
+                                   "factorisation over groups of %d channels (%d float32 pattern "
+                                   "series; the channel sum regrouped: within the float32 bar, "
+                                   "exact for integer-valued data)")
                                   % (fx_g, fx_pat) if fx_g else "channel by channel")},
             "roofline": {"bound": "lds", "achieved": achieved, "peak": lds_roof,
                          "unit": "T adds/s", "frac": achieved / lds_roof if achieved else None,
