@@ -1252,6 +1252,8 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     int e_next = ((kRot || lw == 0) && meta_first < nchunk) ? cht_t[1 + meta_first] : 0;
     auto issue_meta = [&](int k) -> int {
       if (k >= nchunk) return 0;
+      // (timing only, 4096: metadata rows not refreshed after the prologue)
+      if (PDD_DMA_MODES && (dbg & 4096) && k >= MA) return 0;
       if (kRot ? (k % NLW != lw) : (lw != 0)) return 0;
       const int e = k < MA ? cht_t[1 + k] : e_next;
       if (kRot) {
