@@ -1665,7 +1665,12 @@ static const Variant kF32Variants[] = {
                                        //   37.9 ms against 39.4 with 3 buffers)
     {0, false, 4, 4, 4, 8, 8, 2, 2},   // DB 32
     {1, false, 4, 4, 1, 8, 1, 2, 0},   // generic, DB 8
-    {1, false, 4, 1, 1, 1, 1, 2, 0}};  // generic, DB 1 (any span that fits 160 KB)
+    {1, false, 4, 1, 1, 1, 1, 2, 0}    // generic, DB 1 (any span that fits 160 KB)
+#ifdef PDD_SWEEP_DEV
+    , {0, false, 4, 4, 4, 12, 8, 2, 4}  // dev (PDD_SWEEP_VARIANT=4): 12 + 4 waves, DB 48
+    , {0, false, 4, 4, 4, 10, 8, 2, 6}  // dev (5): 10 + 6 waves, DB 40
+#endif
+};
 // 8-bit input: u16 eighths (12 compute + 4 loader waves: with half the
 // compute per staged byte the extra loaders pay off), then the float32-image
 // tilings, then the generic u16 kernel.
@@ -1730,6 +1735,12 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false, int fxs = 0)
     // float32 quarters (the channel sweep's f32 tiling)
     if (v.S == 4 && v.NW == 14 && v.NLW == 2 && v.G == 4 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
       return k_sweep_il<4, 4, 14, 2, 8, 2, false, true, 43>;
+#ifdef PDD_SWEEP_DEV
+    if (v.S == 4 && v.NW == 12 && v.NLW == 4 && v.G == 4 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
+      return k_sweep_il<4, 4, 12, 4, 8, 2, false, true, 43>;
+    if (v.S == 4 && v.NW == 10 && v.NLW == 6 && v.G == 4 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
+      return k_sweep_il<4, 4, 10, 6, 8, 2, false, true, 43>;
+#endif
     return nullptr;
   }
 #define IL(NCW_, NLW_, CC_, NB_)                                                              \
@@ -1747,6 +1758,10 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false, int fxs = 0)
 #endif
   }
   IL(14, 2, 8, 2)
+#ifdef PDD_SWEEP_DEV
+  IL(12, 4, 8, 2)
+  IL(10, 6, 8, 2)
+#endif
   IL(8, 2, 8, 2)
 #undef IL
   return nullptr;
