@@ -258,6 +258,19 @@ def _free_port():
     return p
 
 
+# PDD_BENCH_BACKEND=gloo: rehearse `--gpus N` with N ranks on the GPUs this
+# box has (one here), barriers and the max-over-ranks timing over gloo; the
+# driver's multi-GPU runs use RCCL ("nccl"), one rank per GPU
+_BACKEND = os.environ.get("PDD_BENCH_BACKEND", "nccl")
+
+
+def max_over_ranks(v, dev):
+    """The maximum of a per-rank float over all ranks (RCCL: on the device)."""
+    t = torch.tensor([float(v)], dtype=torch.float64, device=dev if _BACKEND == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def _maybe_spawn(args):
     """`--gpus N` outside torchrun: start N ranks (one per GPU) with
     torch.distributed.run before this process touches the GPU, and exit with
@@ -313,9 +326,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if _BACKEND == "gloo":
+        # rehearsal of the N-rank code path on fewer GPUs (gloo: CPU
+        # barriers/reductions; the ranks share the visible GPUs)
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world > 1 and _BACKEND == "gloo":
+        dist.init_process_group("gloo")
+    elif world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
     import __graft_entry__ as g
@@ -464,9 +483,7 @@ def sweep_bench(args, cfg, rank, world, dev):
         del hpart
         best = min(ms)
         if world > 1:
-            t = torch.tensor([best], device=dev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            best = float(t.item())
+            best = max_over_ranks(best, dev)
         nbytes = part.numel() * part.element_size()
         e2e = {"ms_per_step": best, "value": D * n_out * C / (best * 1e-3),
                "h2d_ms": min(h2d), "h2d_GBs": nbytes / (min(h2d) * 1e-3) / 1e9,
@@ -497,9 +514,7 @@ def sweep_bench(args, cfg, rank, world, dev):
         del hx, hp, xd
     rccl_world = dist.get_world_size() if world > 1 else 1
     if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el = max_over_ranks(el, dev)
     adds_rank_step = rows * cols_rank * C        # one add per samp*ch*DM on this rank
     units_all = D * n_out * C * (world if mode == "timeblock" else 1)
     value = units_all * steps / el
@@ -568,7 +583,8 @@ def sweep_bench(args, cfg, rank, world, dev):
                        "n_out": n_out, "mode": mode,
                        "parallelism": "%s%d" % ({"timeblock": "tb", "timeshard": "ts"}
                                                 .get(mode, "dm"), world),
-                       "rccl_world_size": rccl_world, "plan": plan,
+                       "rccl_world_size": rccl_world if _BACKEND == "nccl" else 0,
+                       "dist_backend": (_BACKEND if world > 1 else None), "plan": plan,
                        "method": (("exact factorisation over groups of %d channels (%d pattern "
                                    "series; plane bit-identical to the channel-by-channel sum)"
                                    if dtype == "u8" else
@@ -972,9 +988,7 @@ def search_bench(args, cfg, rank, world, dev):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el = max_over_ranks(el, dev)
     ms = ev[0].elapsed_time(ev[1]) / args.steps
     byts = 2 * D * n * 4
     achieved = byts / (ms * 1e-3) / 1e9
@@ -1053,9 +1067,7 @@ def stream_bench(args, cfg, rank, world, dev):
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el = max_over_ranks(el, dev)
     units = D * nb * C * args.steps * world
     value = units / el
     lds_roof = N_CU * CLK_GHZ * 1e9 * LDS_B_PER_CLK / 16 * (8 if st.exact else 4) / 1e12
@@ -1152,9 +1164,7 @@ def subband_bench(args, cfg, rank, world, dev):
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el = max_over_ranks(el, dev)
     ms = el / args.steps * 1e3
     line = {
         "metric": "DM-trial samples*channels/sec (node) + % HBM roofline",

@@ -692,8 +692,22 @@ __global__ __launch_bounds__(256) void k_fx_patterns(const uint4* __restrict__ R
 // above reads four rows per pattern element from L2: 4 x 16 B per 16 B
 // written).  gtab: [NG + 1] first pattern of each group, then [NG] x {lo,
 // hi} = the group's min(0, r) / max(0, r) over its patterns (hi - lo <=
-// kFxRspan, checked by the plan).
+// kFxRspan, checked by the plan), then [n_pat] x {first, last - nR}: the
+// pattern row's elements stage 2 reads (fx_build): kFxE-element blocks
+// outside that range are not written.
 constexpr int kFxE = 512, kFxRspan = 512;
+// The group's pattern descriptors 64 at a time, one wave-wide load: lane i
+// holds pattern pb + i's relative shifts and row range (fx_build), which the
+// pattern loops take by v_readlane -- no dependent scalar loads per pattern.
+struct FxBatch {
+  int y, z, w, lo, hi;
+};
+__device__ __forceinline__ FxBatch fx_batch(const int4* __restrict__ pat, const int* __restrict__ rng,
+                                            int pb, int p1) {
+  const int pl = min(pb + (int)(threadIdx.x & 63), p1 - 1);
+  const int4 q = pat[pl];
+  return {q.y, q.z, q.w, rng[2 * pl], rng[2 * pl + 1]};
+}
 __global__ __launch_bounds__(256) void k_fx_patterns_lds(const uint4* __restrict__ R, int64_t nR,
                                                          const int4* __restrict__ pat,
                                                          const int* __restrict__ gtab, int NG,
@@ -711,17 +725,25 @@ __global__ __launch_bounds__(256) void k_fx_patterns_lds(const uint4* __restrict
       L[k * W + e] = (i >= 0 && i < nR) ? r0[(int64_t)k * nR + i] : make_uint4(0u, 0u, 0u, 0u);
     }
   __syncthreads();
-  for (int p = p0; p < p1; ++p) {
-    const int4 q = pat[p];
+  const int* rng = gtab + 3 * NG + 1;
+  for (int pb = p0; pb < p1; pb += 64) {
+    const FxBatch B = fx_batch(pat, rng, pb, p1);
+    for (int i = 0; i < min(64, p1 - pb); ++i) {
+      const int p = pb + i;
+      const int4 q = make_int4(0, __builtin_amdgcn_readlane(B.y, i), __builtin_amdgcn_readlane(B.z, i),
+                               __builtin_amdgcn_readlane(B.w, i));
+      const int64_t jlo = __builtin_amdgcn_readlane(B.lo, i), jhi = nR + __builtin_amdgcn_readlane(B.hi, i);
+      if (j0 >= jhi || j0 + kFxE <= jlo) continue;  // no trial of p reads this block
 #pragma unroll
-    for (int e = threadIdx.x; e < kFxE; e += 256) {
-      const int64_t j = j0 + e;
-      if (j >= nR) break;
-      const uint4 a = L[e - lo], b = L[W + e - lo + q.y];
-      const uint4 c = fx > 2 ? L[2 * W + e - lo + q.z] : make_uint4(0u, 0u, 0u, 0u);
-      const uint4 d = fx > 3 ? L[3 * W + e - lo + q.w] : make_uint4(0u, 0u, 0u, 0u);
-      P[(int64_t)p * nR + j] = make_uint4(a.x + b.x + c.x + d.x, a.y + b.y + c.y + d.y,
-                                          a.z + b.z + c.z + d.z, a.w + b.w + c.w + d.w);
+      for (int e = threadIdx.x; e < kFxE; e += 256) {
+        const int64_t j = j0 + e;
+        if (j >= nR) break;  // (a block's elements outside [jlo, jhi): written, unread)
+        const uint4 a = L[e - lo], b = L[W + e - lo + q.y];
+        const uint4 c = fx > 2 ? L[2 * W + e - lo + q.z] : make_uint4(0u, 0u, 0u, 0u);
+        const uint4 d = fx > 3 ? L[3 * W + e - lo + q.w] : make_uint4(0u, 0u, 0u, 0u);
+        P[(int64_t)p * nR + j] = make_uint4(a.x + b.x + c.x + d.x, a.y + b.y + c.y + d.y,
+                                            a.z + b.z + c.z + d.z, a.w + b.w + c.w + d.w);
+      }
     }
   }
 }
@@ -733,7 +755,7 @@ __global__ __launch_bounds__(256) void k_fx_patterns_lds(const uint4* __restrict
 // pattern of the group as k_fx_patterns_lds does.  Saves the image's write
 // and read, and the interleave launch, per segment (the per-rank work of a
 // DM-sharded step that does not shrink with the world size).
-template <typename InT, bool NT = false>
+template <typename InT, int FXG>
 __global__ __launch_bounds__(256) void k_fx_patterns_x(const InT* __restrict__ x, InLayout lay,
                                                        int64_t N, int64_t base, int64_t Qs,
                                                        int64_t nR, int pad_mode,
@@ -751,8 +773,8 @@ __global__ __launch_bounds__(256) void k_fx_patterns_x(const InT* __restrict__ x
   // (every block but the segment's edges) loads without per-sample tests
   const int64_t s_lo = base + j0 + lo, s_hi = s_lo + W - 1 + 7 * Qs;
   const bool inner = j0 + lo >= 0 && j0 + lo + W <= nR && s_lo >= 0 && s_hi < N;
-  for (int k = 0; k < fx; ++k) {
-    const int c = g * fx + k;
+  for (int k = 0; k < FXG; ++k) {
+    const int c = g * FXG + k;
     const uint32_t pv = (pad_mode == PDD_PAD_VALUE) ? (uint32_t)padvals[c] : 0u;
     if (inner) {
       for (int e = threadIdx.x; e < W; e += 256) {
@@ -781,21 +803,22 @@ __global__ __launch_bounds__(256) void k_fx_patterns_x(const InT* __restrict__ x
     }
   }
   __syncthreads();
-  for (int p = p0; p < p1; ++p) {
-    const int4 q = pat[p];
+  const int* rng = gtab + 3 * NG + 1;
+  for (int pb = p0; pb < p1; pb += 64) {
+    const FxBatch B = fx_batch(pat, rng, pb, p1);
+    for (int i = 0; i < min(64, p1 - pb); ++i) {
+      const int p = pb + i;
+      const int4 q = make_int4(0, __builtin_amdgcn_readlane(B.y, i), __builtin_amdgcn_readlane(B.z, i),
+                               __builtin_amdgcn_readlane(B.w, i));
+      const int64_t jlo = __builtin_amdgcn_readlane(B.lo, i), jhi = nR + __builtin_amdgcn_readlane(B.hi, i);
+      if (j0 >= jhi || j0 + kFxE <= jlo) continue;  // no trial of p reads this block
 #pragma unroll
-    for (int e = threadIdx.x; e < kFxE; e += 256) {
-      const int64_t j = j0 + e;
-      if (j >= nR) break;
-      const uint4 a = L[e - lo], b = L[W + e - lo + q.y];
-      const uint4 c = fx > 2 ? L[2 * W + e - lo + q.z] : make_uint4(0u, 0u, 0u, 0u);
-      const uint4 d = fx > 3 ? L[3 * W + e - lo + q.w] : make_uint4(0u, 0u, 0u, 0u);
-      if constexpr (NT) {
-        typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
-        const v4u_t r = {a.x + b.x + c.x + d.x, a.y + b.y + c.y + d.y, a.z + b.z + c.z + d.z,
-                         a.w + b.w + c.w + d.w};
-        __builtin_nontemporal_store(r, reinterpret_cast<v4u_t*>(P) + ((int64_t)p * nR + j));
-      } else {
+      for (int e = threadIdx.x; e < kFxE; e += 256) {
+        const int64_t j = j0 + e;
+        if (j >= nR) break;  // (a block's elements outside [jlo, jhi): written, unread)
+        const uint4 a = L[e - lo], b = L[W + e - lo + q.y];
+        const uint4 c = FXG > 2 ? L[2 * W + e - lo + q.z] : make_uint4(0u, 0u, 0u, 0u);
+        const uint4 d = FXG > 3 ? L[3 * W + e - lo + q.w] : make_uint4(0u, 0u, 0u, 0u);
         P[(int64_t)p * nR + j] = make_uint4(a.x + b.x + c.x + d.x, a.y + b.y + c.y + d.y,
                                             a.z + b.z + c.z + d.z, a.w + b.w + c.w + d.w);
       }
@@ -810,6 +833,7 @@ __global__ __launch_bounds__(256) void k_fx_patterns_x(const InT* __restrict__ x
 // then adds pattern series instead of channels -- the reference's float64
 // channel sum regrouped, within the float32 parity bar (and exact for
 // integer-valued data).  Pads as k_interleave: value (per channel) / rotate.
+template <int FXG>
 __global__ __launch_bounds__(256) void k_fx_patterns_xf(const float* __restrict__ x, InLayout lay,
                                                         int64_t N, int64_t base, int64_t Qs,
                                                         int64_t nR, int pad_mode,
@@ -826,8 +850,8 @@ __global__ __launch_bounds__(256) void k_fx_patterns_xf(const float* __restrict_
   // interior blocks load without per-sample tests (as k_fx_patterns_x)
   const int64_t s_lo = base + j0 + lo, s_hi = s_lo + W - 1 + 3 * Qs;
   const bool inner = j0 + lo >= 0 && j0 + lo + W <= nR && s_lo >= 0 && s_hi < N;
-  for (int k = 0; k < fx; ++k) {
-    const int c = g * fx + k;
+  for (int k = 0; k < FXG; ++k) {
+    const int c = g * FXG + k;
     const float pv = (pad_mode == PDD_PAD_VALUE) ? padvals[c] : 0.f;
     if (inner) {
       for (int e = threadIdx.x; e < W; e += 256) {
@@ -852,21 +876,29 @@ __global__ __launch_bounds__(256) void k_fx_patterns_xf(const float* __restrict_
     }
   }
   __syncthreads();
-  for (int p = p0; p < p1; ++p) {
-    const int4 q = pat[p];
+  const int* rng = gtab + 3 * NG + 1;
+  for (int pb = p0; pb < p1; pb += 64) {
+    const FxBatch B = fx_batch(pat, rng, pb, p1);
+    for (int i = 0; i < min(64, p1 - pb); ++i) {
+      const int p = pb + i;
+      const int4 q = make_int4(0, __builtin_amdgcn_readlane(B.y, i), __builtin_amdgcn_readlane(B.z, i),
+                               __builtin_amdgcn_readlane(B.w, i));
+      const int64_t jlo = __builtin_amdgcn_readlane(B.lo, i), jhi = nR + __builtin_amdgcn_readlane(B.hi, i);
+      if (j0 >= jhi || j0 + kFxE <= jlo) continue;  // (as k_fx_patterns_lds)
 #pragma unroll
-    for (int e = threadIdx.x; e < kFxE; e += 256) {
-      const int64_t j = j0 + e;
-      if (j >= nR) break;
-      float4 s = Lf[e - lo];
-      const float4 b = Lf[W + e - lo + q.y];
-      s.x += b.x; s.y += b.y; s.z += b.z; s.w += b.w;
-      if (fx > 2) {
-        const float4 c = Lf[2 * W + e - lo + q.z], d = Lf[3 * W + e - lo + q.w];
-        s.x += c.x; s.y += c.y; s.z += c.z; s.w += c.w;
-        s.x += d.x; s.y += d.y; s.z += d.z; s.w += d.w;
+      for (int e = threadIdx.x; e < kFxE; e += 256) {
+        const int64_t j = j0 + e;
+        if (j >= nR) break;  // (a block's elements outside [jlo, jhi): written, unread)
+        float4 s = Lf[e - lo];
+        const float4 b = Lf[W + e - lo + q.y];
+        s.x += b.x; s.y += b.y; s.z += b.z; s.w += b.w;
+        if constexpr (FXG > 2) {
+          const float4 c = Lf[2 * W + e - lo + q.z], d = Lf[3 * W + e - lo + q.w];
+          s.x += c.x; s.y += c.y; s.z += c.z; s.w += c.w;
+          s.x += d.x; s.y += d.y; s.z += d.z; s.w += d.w;
+        }
+        P[(int64_t)p * nR + j] = s;
       }
-      P[(int64_t)p * nR + j] = s;
     }
   }
 }
@@ -2039,6 +2071,15 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
                          t_base + lo + x_off, Qs, nR, pad_mode, padvals, R);
     if (hipGetLastError() != hipSuccess) { rc = -3; break; }
     if (p->fx) {
+      // PDD_SWEEP_POISON=1 (a parity-test switch): the pattern rows are filled
+      // with 0xFF bytes first, so a sum that read an element stage 1 did not
+      // write (the per-pattern ranges of fx_build) shows as a NaN / an
+      // overflowed lane instead of a stale-but-plausible value
+      if (getenv("PDD_SWEEP_POISON") && atoi(getenv("PDD_SWEEP_POISON")) &&
+          hipMemsetAsync(P, 0xFF, (size_t)(p->n_pat * nR) * sizeof(uint4), st) != hipSuccess) {
+        rc = -3;
+        break;
+      }
       if (hipMemsetAsync(P + p->n_pat * nR, 0, (size_t)nR * sizeof(uint4), st) != hipSuccess) {
         rc = -3;
         break;
@@ -2047,27 +2088,24 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
       const dim3 gp((unsigned)NG, (unsigned)cdiv(nR, kFxE));
       const size_t lds_p = (size_t)(p->fx * (kFxE + p->fx_rspan)) * sizeof(uint4);
       const int64_t b0 = t_base + lo + x_off;
-#ifdef PDD_SWEEP_DEV
-      static const bool s1_nt = getenv("PDD_FX_S1_NT") && atoi(getenv("PDD_FX_S1_NT"));
-#else
-      constexpr bool s1_nt = false;
-#endif
-      if (fx_direct && p->dtype == PDD_U8 && s1_nt) {
-        hipLaunchKernelGGL((k_fx_patterns_x<uint8_t, true>), gp, dim3(256), lds_p, st, (const uint8_t*)x,
-                           lay, N, b0, Qs, nR, pad_mode, padvals, (const int4*)p->d_pat, p->d_gtab, NG,
-                           p->fx, P);
-      } else if (fx_direct && p->dtype == PDD_F32) {
-        hipLaunchKernelGGL(k_fx_patterns_xf, gp, dim3(256), lds_p, st, (const float*)x, lay, N, b0,
-                           Qs, nR, pad_mode, padvals, (const int4*)p->d_pat, p->d_gtab, NG, p->fx,
-                           (float4*)P);
+      // (stage-1 kernels are instanced per group size: fx_build makes groups of 2 or 4)
+#define PDD_FX_S1(K2, K4, ...)                                                     \
+  do {                                                                             \
+    if (p->fx == 4) hipLaunchKernelGGL(K4, gp, dim3(256), lds_p, st, __VA_ARGS__); \
+    else hipLaunchKernelGGL(K2, gp, dim3(256), lds_p, st, __VA_ARGS__);            \
+  } while (0)
+      if (fx_direct && p->dtype == PDD_F32) {
+        PDD_FX_S1(k_fx_patterns_xf<2>, k_fx_patterns_xf<4>, (const float*)x, lay, N, b0, Qs, nR,
+                  pad_mode, padvals, (const int4*)p->d_pat, p->d_gtab, NG, p->fx, (float4*)P);
       } else if (fx_direct && p->dtype == PDD_U8) {
-        hipLaunchKernelGGL(k_fx_patterns_x<uint8_t>, gp, dim3(256), lds_p, st, (const uint8_t*)x, lay,
-                           N, b0, Qs, nR, pad_mode, padvals, (const int4*)p->d_pat, p->d_gtab, NG,
-                           p->fx, P);
+        PDD_FX_S1((k_fx_patterns_x<uint8_t, 2>), (k_fx_patterns_x<uint8_t, 4>), (const uint8_t*)x,
+                  lay, N, b0, Qs, nR, pad_mode, padvals, (const int4*)p->d_pat, p->d_gtab, NG, p->fx,
+                  P);
       } else if (fx_direct) {
-        hipLaunchKernelGGL(k_fx_patterns_x<uint16_t>, gp, dim3(256), lds_p, st, (const uint16_t*)x,
-                           lay, N, b0, Qs, nR, pad_mode, padvals, (const int4*)p->d_pat, p->d_gtab,
-                           NG, p->fx, P);
+        PDD_FX_S1((k_fx_patterns_x<uint16_t, 2>), (k_fx_patterns_x<uint16_t, 4>), (const uint16_t*)x,
+                  lay, N, b0, Qs, nR, pad_mode, padvals, (const int4*)p->d_pat, p->d_gtab, NG, p->fx,
+                  P);
+#undef PDD_FX_S1
       } else if (p->d_gtab) {
         hipLaunchKernelGGL(k_fx_patterns_lds, gp, dim3(256), lds_p, st, (const uint4*)R, nR,
                            (const int4*)p->d_pat, p->d_gtab, NG, p->fx, P);
@@ -2169,6 +2207,33 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
     }
     while (g < NG) T.gtab[(size_t)(++g)] = (int)T.n_pat;
     if (!fits) T.gtab.clear();
+  }
+  if (!T.gtab.empty()) {
+    // then [n_pat] x {first, last - nR} = the pattern row's elements stage 2
+    // reads: trials of pattern p have base shifts b in [bmin_p, bmax_p], so
+    // its windows cover elements [bmin_p - lo, Qs + bmax_p - lo) of a
+    // segment's row (nR = Qs + hi - lo + 64; lo = min(0, min bin), hi =
+    // max(0, max bin)); stage 1 skips its kFxE-element blocks outside them
+    // (5-10% of the image's bytes are delay overhang no trial of the pattern
+    // reads)
+    int32_t lo_all = 0, hi_all = 0;
+    for (int64_t i = 0; i < D * C; ++i) {
+      lo_all = std::min(lo_all, tab[i]);
+      hi_all = std::max(hi_all, tab[i]);
+    }
+    const size_t o = (size_t)(3 * NG + 1);
+    T.gtab.resize(o + 2 * (size_t)T.n_pat);
+    for (int64_t p = 0; p < T.n_pat; ++p) {
+      T.gtab[o + 2 * p] = INT32_MAX;
+      T.gtab[o + 2 * p + 1] = INT32_MIN;
+    }
+    for (int64_t d = 0; d < D; ++d)
+      for (int64_t g = 0; g < NG; ++g) {
+        const size_t q = o + 2 * (size_t)pid[(size_t)(d * NG + g)];
+        const int32_t b = tab[d * C + g * fx];
+        T.gtab[q] = std::min(T.gtab[q], b - lo_all);
+        T.gtab[q + 1] = std::max(T.gtab[q + 1], b - hi_all - 64);
+      }
   }
   // float32 patterns are built only by the LDS stage 1 from the input rows
   // (k_fx_patterns_xf: float adds)
@@ -2568,9 +2633,11 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
         if (e == hipSuccess && !T.gtab.empty()) e = hipMalloc(&p->d_gtab, T.gtab.size() * sizeof(int));
         if (e == hipSuccess && !T.gtab.empty())
           e = hipMemcpy(p->d_gtab, T.gtab.data(), T.gtab.size() * sizeof(int), hipMemcpyHostToDevice);
-        for (const void* kf : {(const void*)k_fx_patterns_lds, (const void*)k_fx_patterns_x<uint8_t>,
-                               (const void*)k_fx_patterns_x<uint16_t>, (const void*)k_fx_patterns_xf,
-                               (const void*)k_fx_patterns_x<uint8_t, true>})
+        for (const void* kf :
+             {(const void*)k_fx_patterns_lds, (const void*)k_fx_patterns_x<uint8_t, 2>,
+              (const void*)k_fx_patterns_x<uint8_t, 4>, (const void*)k_fx_patterns_x<uint16_t, 2>,
+              (const void*)k_fx_patterns_x<uint16_t, 4>, (const void*)k_fx_patterns_xf<2>,
+              (const void*)k_fx_patterns_xf<4>})
           if (e == hipSuccess && !T.gtab.empty())
             e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)(4 * (kFxE + kFxRspan) * sizeof(uint4)));

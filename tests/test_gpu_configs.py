@@ -127,12 +127,13 @@ def test_config3_sweep_oracle_rows(gpu):
     ds.close()
 
 
-def test_northstar_g2_plane(gpu):
+def test_northstar_g2_plane(gpu, monkeypatch):
     """The north-star grid (4096 ch, 2048 DMs 0-1000, DDplan2b.py:168
     arange grid spacing) at N = 2^18: the planner picks the factorised sweep
     over groups of 2 channels (the per-lane staging instance of k_sweep_il),
     its plane equals the channel-by-channel kernel bit for bit, and sampled
     rows equal the oracle's per-trial channel sums."""
+    monkeypatch.setenv("PDD_SWEEP_POISON", "1")  # (tests/test_gpu_factor.py)
     import torch
     from oracle import spectra_oracle as orc
     from pypulsar_amd import _lib
@@ -158,13 +159,14 @@ def test_northstar_g2_plane(gpu):
     sw.close()
 
 
-def test_config3_timeshard_8_ranks(gpu):
+def test_config3_timeshard_8_ranks(gpu, monkeypatch):
     """The 8-rank TIME-sharded configs[3] step (TimeShardedSweep(world=8,
     rank=r), bench.py's N > 1 default) at N = 2^18 on one GPU: each rank
     corner-turns its own input spectra (its plane columns + the max-delay
     overlap) and sweeps the whole 4096-DM grid over its columns with its own
     (factorised) plan; the 8 column blocks concatenate to the one-shot plane
     bit for bit, and sampled rows equal the oracle."""
+    monkeypatch.setenv("PDD_SWEEP_POISON", "1")  # (tests/test_gpu_factor.py)
     import torch
     from oracle import spectra_oracle as orc
     from pypulsar_amd.sharding import TimeShardedSweep

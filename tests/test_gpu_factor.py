@@ -14,6 +14,16 @@ from oracle import spectra_oracle as orc
 DT = 64e-6
 
 
+@pytest.fixture(autouse=True)
+def poison_patterns(monkeypatch):
+    """Every factorised sweep here first fills its pattern image with 0xFF
+    bytes (PDD_SWEEP_POISON): stage 1 writes only the row elements each
+    pattern's trials read (fx_build's per-pattern ranges), so a sum reading
+    an unwritten element turns into a NaN / an overflowed lane, not a stale
+    value that happens to match."""
+    monkeypatch.setenv("PDD_SWEEP_POISON", "1")
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("pad", [0, 7, "rotate"])
 @pytest.mark.parametrize("descending", [True, False])

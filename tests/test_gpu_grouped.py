@@ -175,12 +175,13 @@ def test_sweep_ds_fused_downsample(gpu, ds, padval, layout):
 @pytest.mark.parametrize("ds", [2, 3, 4])
 @pytest.mark.parametrize("padval", [0, 17, "rotate"])
 @pytest.mark.parametrize("factor", ["force4", "force2", True])
-def test_sweep_ds_factorised(gpu, ds, padval, factor):
+def test_sweep_ds_factorised(gpu, ds, padval, factor, monkeypatch):
     """sweep_ds (and so DDplanExecutor's one-stage steps at downsamp 2..4) on
     a dtype='u16' plan that IS factorised: the interleave pre-pass co-adds
     the raw rows, stage 1 builds the patterns from that image, and the plane
     equals the oracle's Spectra.downsample + per-trial sweep bit for bit.
     factor=True: whatever the planner picks for this grid."""
+    monkeypatch.setenv("PDD_SWEEP_POISON", "1")  # (tests/test_gpu_factor.py)
     import torch
     from pypulsar_amd import _lib
     from pypulsar_amd.sweep import DMSweep
