@@ -1088,7 +1088,7 @@ __host__ __device__ constexpr int il_meta_bytes(int nbuf, int cc, int db) {
 #ifndef PDD_FX_GJ
 #define PDD_FX_GJ PDD_IL_GJ
 #endif
-template <int GT = PDD_IL_GT, int GJ = PDD_IL_GJ>
+template <int GT = PDD_IL_GT, int GJ = PDD_IL_GJ, bool XI = false>
 __device__ __forceinline__ void il_tile_of(int bid, int n_tblk, int n_dblk, int dbg, int& dblk,
                                            int& tblk) {
   const int total = n_tblk * n_dblk;
@@ -1121,7 +1121,17 @@ __device__ __forceinline__ void il_tile_of(int bid, int n_tblk, int n_dblk, int 
   const int gj = min(GJ, n_dblk - jg * GJ);  // trial blocks in this group
   r -= jg * gtb * GJ;
   dblk = jg * GJ + r % gj;
-  tblk = x * TX + band * GT + r / gj;
+  if constexpr (XI) {
+    // the eight XCDs' k-th bands adjacent in time: band b of XCD x is global
+    // band 8b + x (the last, possibly shorter, bands side by side), so the
+    // windows two neighbouring bands share are fetched from HBM once, into
+    // the Infinity Cache, while both XCDs run them (north star 95.4 -> 91.9
+    // ms per launch; configs[3] unchanged, 129.8 / 129.4)
+    const int nb = (TX + GT - 1) / GT;
+    tblk = (band < nb - 1 ? (band * 8 + x) * GT : 8 * (nb - 1) * GT + x * gtb) + r / gj;
+  } else {
+    tblk = x * TX + band * GT + r / gj;
+  }
 }
 
 // Eight consecutive metadata rows' window fields {bmin, span, offset,
@@ -1196,7 +1206,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
 #define IL_TILE_SETUP                                                         \
   int dblk, tblk;                                                             \
   const int grp = tile / per_grp;                                             \
-  il_tile_of<FX ? PDD_FX_GT : PDD_IL_GT, FX ? PDD_FX_GJ : PDD_IL_GJ>(           \
+  il_tile_of<FX ? PDD_FX_GT : PDD_IL_GT, FX ? PDD_FX_GJ : PDD_IL_GJ, FX>(           \
       tile - grp * per_grp, n_tblk, n_dblk, dbg, dblk, tblk);                 \
   if (PDD_DMA_MODES && (dbg & 384)) tblk = (dbg & 128) ? 0 : (tblk & 7);          \
   const float4* R = R0 + (int64_t)grp * C * nR;                               \
@@ -1230,7 +1240,20 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     if constexpr (FXS & 1) {
       // lane i = window i: its source, LDS address and piece count in one
       // pass, then this loader's windows (i = first mod step) from SGPRs
-      const uint64_t sv = (uint64_t)(R + (int64_t)(rec.w & 0xfffff) * nR + (t0 + rec.x - lo));
+      int64_t rstride = nR, rrow = rec.w & 0xfffff;
+      // (timing only, wrong results: 8192 -- every window from rows 0..15;
+      // 16384 -- rows 256 elements apart: the address spread of the windows)
+      if (PDD_DMA_MODES && (dbg & 8192)) rrow &= 15;
+      if (PDD_DMA_MODES && (dbg & 16384)) rstride = 256;
+      int64_t toff = t0;
+      // (32768: rows 256 elements apart WITHIN a time tile's own region --
+      // time tile t's windows at ((t mod 256) * 32768 rows) * 256 elements:
+      // the tile's address spread of a time-blocked layout, its data volume)
+      if (PDD_DMA_MODES && (dbg & 32768)) {
+        rstride = 256;
+        toff = (int64_t)((t0 / Tq) % 256) * 32768 * 256;
+      }
+      const uint64_t sv = (uint64_t)(R + rrow * rstride + (toff + rec.x - lo));
       const uint32_t dv = img_lds + (uint32_t)((b * buf_e + rec.z) * 16);
       const int qv = (rec.y + 63) >> 6;
       for (int i = first; i < nw; i += step) {
