@@ -293,3 +293,39 @@ def test_timeshard_rehearsal_ranks_concatenate_to_one_shot(world):
         cols.append(ts(block[lo:hi].contiguous()).numpy().copy())
     want = orc.sweep_plane(_data(C, N).astype(np.float64), tab)
     np.testing.assert_array_equal(np.concatenate(cols, axis=1).astype(np.float64), want)
+
+
+def _bench_reduce_worker(rank, world, port, q):
+    # bench.py's max-over-ranks timing under the gloo rehearsal backend
+    # (PDD_BENCH_BACKEND=gloo: `--gpus N` ranks sharing fewer GPUs)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["PDD_BENCH_BACKEND"] = "gloo"
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "bench_rehearsal", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                        "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, bench.max_over_ranks(1.5 * rank + 0.25, None)))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_max_over_ranks_gloo():
+    """bench.py's per-rank timing reduction (the MAX over ranks of the timed
+    region, rank 0 prints the line) over gloo, world size 3."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_reduce_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(3))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got == {0: 3.25, 1: 3.25, 2: 3.25}
