@@ -695,10 +695,7 @@ __global__ __launch_bounds__(256) void k_fx_patterns(const uint4* __restrict__ R
 // kFxRspan, checked by the plan), then [n_pat] x {first, last - nR}: the
 // pattern row's elements stage 2 reads (fx_build): kFxE-element blocks
 // outside that range are not written.
-#ifndef PDD_FXE
-#define PDD_FXE 512  // (developer builds: other stage-1 block lengths)
-#endif
-constexpr int kFxE = PDD_FXE, kFxRspan = 512;
+constexpr int kFxE = 512, kFxRspan = 512;
 // The group's pattern descriptors 64 at a time, one wave-wide load: lane i
 // holds pattern pb + i's relative shifts and row range (fx_build), which the
 // pattern loops take by v_readlane -- no dependent scalar loads per pattern.
