@@ -1081,12 +1081,16 @@ __host__ __device__ constexpr int il_meta_bytes(int nbuf, int cc, int db) {
 #define PDD_IL_GJ 4
 #endif
 // factorised tiles (their own tile-order shape: trial blocks of one time tile
-// share pattern rows, so the shapes are measured separately)
+// share pattern rows, so the shapes are measured separately).  With the
+// XCD-adjacent bands, groups of 4 time tiles x 2 trial blocks: configs[3]
+// stage 2 129.2 -> 120.9 ms per launch, north star 91.9 -> 90.0 (same box,
+// twice each; 8 x 4 / 8 x 2 / 6 x 2 / 4 x 4 / 4 x 1 / 8 x 1 / 2 x 4 / 2 x 2 /
+// 8 x 8 in DESIGN.md §4)
 #ifndef PDD_FX_GT
-#define PDD_FX_GT PDD_IL_GT
+#define PDD_FX_GT 4
 #endif
 #ifndef PDD_FX_GJ
-#define PDD_FX_GJ PDD_IL_GJ
+#define PDD_FX_GJ 2
 #endif
 template <int GT = PDD_IL_GT, int GJ = PDD_IL_GJ, bool XI = false>
 __device__ __forceinline__ void il_tile_of(int bid, int n_tblk, int n_dblk, int dbg, int& dblk,
