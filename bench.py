@@ -230,22 +230,25 @@ def _cpu_pool(x, freqs, dt, dms, orc, workers=None, ntrials=None, cblk=64):
                        "C-order, %.1f s" % (ntrials, cblk, workers, el))
 
 
-def load_pmc(path, key, plan=None):
-    """profiles/pmc_sweep.json[key] if it was measured on THIS build: the
-    entry's source digest (scripts/collect_profiles.py) must equal the
-    library sources' digest and its sweep plan the running plan; stale
-    counters are refused (None)."""
+def load_pmc(path, key, plan=None, ctx=None):
+    """profiles/pmc_sweep.json[key] if it was measured on THIS binary and run:
+    the entry's source digest (scripts/collect_profiles.py) must equal the
+    digest compiled into the LOADED libpdd.so, its sweep plan the running
+    plan and its run context (mode, world size, launches per step = columns
+    per launch) this run's; anything else is refused (None)."""
     try:
         with open(path) as f:
             e = json.load(f).get(key)
+        if not isinstance(e, dict):
+            return None
+        from pypulsar_amd._lib import loaded_digest
+        if e.get("src_digest") != loaded_digest():
+            return None
     except Exception:
         return None
-    if not isinstance(e, dict):
-        return None
-    from pypulsar_amd._lib import source_digest
-    if e.get("src_digest") != source_digest():
-        return None
     if plan is not None and e.get("plan") is not None and e.get("plan") != plan:
+        return None
+    if ctx is not None and e.get("ctx") != ctx:
         return None
     return e
 
@@ -544,9 +547,16 @@ def sweep_bench(args, cfg, rank, world, dev):
         pmc_key = "northstar"
     plan = sw.info(1 if dtype == "u8" else 0) if sw is not None else None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_sweep.json")
-    pmc = load_pmc(pmc_path, pmc_key, plan)
+    lps = launches / steps if launches else None
+    ctx = {"mode": mode, "world": world, "launches_per_step": lps}
+    pmc = load_pmc(pmc_path, pmc_key, plan, ctx)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
-    pmc1 = load_pmc(pmc_path, pmc_key + "_stage1", plan) if fx_g else None
+    pmc1 = load_pmc(pmc_path, pmc_key + "_stage1", plan, ctx) if fx_g else None
+    # per step: the sweep kernel's (and stage 1's) counter bytes per launch x
+    # launches per step, against the algorithmic bytes (input once + plane once)
+    traffic_step = None
+    if traffic and lps:
+        traffic_step = (traffic + (pmc1.get("hbm_bytes_per_launch") if pmc1 else 0.0)) * lps
 
     if rank == 0:
         line = {
@@ -604,6 +614,11 @@ def sweep_bench(args, cfg, rank, world, dev):
                          if traffic else "no PMC entry measured on this build (source digest / "
                                          "plan mismatch): traffic not reported",
                          "traffic_stage1": pmc1.get("hbm_bytes_per_launch") if pmc1 else None,
+                         "traffic_unit": "HBM-side bytes per launch (traffic: this kernel; "
+                                         "traffic_stage1: the factorised stage 1)",
+                         "traffic_per_step": traffic_step,
+                         "algorithmic_bytes_per_step": uniq_bytes,
+                         "traffic_ratio": traffic_step / uniq_bytes if traffic_step else None,
                          "kernel": ("pdd::k_sweep_il (factorised stage 2)" if fx_g
                                     else "pdd::k_sweep_il"), "kernel_ms_per_launch":
                              kern_ms / launches if launches else None,

@@ -44,6 +44,12 @@ enum { PDD_LAYOUT_TIME_MAJOR = 0, /* [nspec][nchan], filterbank file order */
 
 int pdd_version(void);
 const char* pdd_last_error(void);
+/* Identity of this build: the 16-hex-digit digest of the HIP sources and
+ * compile flags the library was built from (pypulsar_amd/_digest.py computes
+ * the same from a source tree).  The Python host refuses a library whose
+ * digest differs from its sources, and profiling evidence is stamped with it,
+ * so counters are only reported for the binary that produced them. */
+const char* pdd_source_digest(void);
 /* Free the device scratch the library keeps per (device, stream, calling host
  * thread) -- sweep images, partial sums; synchronises the device.  Optional:
  * the next call that needs scratch allocates it again.  Scratch is keyed by
@@ -281,6 +287,15 @@ int pdd_sweep_plan_info(const pdd_sweep_plan* plan, int64_t* info /*[8]*/);
  * fewer conversions; a sample above it gives wrong sums.  E.g. the
  * zero_dm_filter.py:30-39 uint8-wrap image co-added by 2 is <= 510. */
 int pdd_sweep_plan_set_input_max(pdd_sweep_plan* plan, int max_value);
+/* Test switches of a plan (parity tests and the C-ABI driver; both default
+ * off).  poison: factorised plans fill their pattern image with 0xFF bytes
+ * before stage 1 of every segment, so a stage-2 read of an element stage 1
+ * did not write shows as a NaN / overflowed lane.  segment_bytes > 0: the
+ * scratch budget of one time segment (default: 16 GiB, 80 GiB for factorised
+ * plans, capped by free device memory), to run the multi-segment path on
+ * small blocks. */
+int pdd_sweep_plan_set_poison(pdd_sweep_plan* plan, int on);
+int pdd_sweep_plan_set_segment_bytes(pdd_sweep_plan* plan, int64_t bytes);
 int pdd_sweep_plan_destroy(pdd_sweep_plan* plan);
 /* Measurement hooks (bench.py): with timing on, every sweep-kernel launch
  * of pdd_sweep_execute(_grouped) -- not the interleave pre-pass -- is

@@ -11,12 +11,16 @@ import os
 
 import torch  # noqa: F401  (load torch's HIP runtime before libpdd.so)
 
+from . import _digest
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpdd.so")
 # developer builds (-DPDD_SWEEP_DEV, scripts/build_dev.sh) are loaded from
-# PDD_DEV_LIB for timing experiments; production runs never set it
-if os.environ.get("PDD_DEV_LIB"):
-    LIB_PATH = os.environ["PDD_DEV_LIB"]
+# PDD_DEV_LIB for timing experiments (no digest check); production runs
+# never set it
+_DEV_LIB = os.environ.get("PDD_DEV_LIB")
+if _DEV_LIB:
+    LIB_PATH = _DEV_LIB
 
 # element types / modes (include/pdd.h)
 F32, U8, U16 = 0, 1, 2
@@ -42,24 +46,15 @@ EXPORTS = (
     "pdd_sp_search", "pdd_psrfits_subints", "pdd_downsample_u8", "pdd_sweep_timing_read",
     "pdd_sweep_execute_ex", "pdd_zdm_int_downsample", "pdd_downsample_u8_u16",
     "pdd_sweep_execute_ds", "pdd_subband_chain", "pdd_scratch_release",
-    "pdd_sweep_plan_create_ex", "pdd_sweep_plan_factor",
+    "pdd_sweep_plan_create_ex", "pdd_sweep_plan_factor", "pdd_source_digest",
+    "pdd_sweep_plan_set_poison", "pdd_sweep_plan_set_segment_bytes",
 )
 
 
 def source_digest():
-    """sha256 (first 16 hex digits) of the HIP sources libpdd.so is built
-    from.  Profiling evidence (profiles/pmc_sweep.json) is stamped with it, so
-    bench.py can refuse counters measured on a different build."""
-    import hashlib
-    csrc = os.path.join(_HERE, "csrc")
-    h = hashlib.sha256()
-    names = sorted(n for n in os.listdir(csrc) if n.endswith((".hip", ".h")))
-    for n in names:
-        with open(os.path.join(csrc, n), "rb") as f:
-            h.update(n.encode() + b"\0" + f.read())
-    with open(os.path.join(os.path.dirname(_HERE), "include", "pdd.h"), "rb") as f:
-        h.update(b"pdd.h\0" + f.read())
-    return h.hexdigest()[:16]
+    """Digest of the library sources + build flags in this tree
+    (pypulsar_amd/_digest.py); a loaded library must carry the same."""
+    return _digest.source_digest()
 
 
 class PddLibraryMissing(RuntimeError):
@@ -75,6 +70,9 @@ _lib = None
 _vp, _i64, _int = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
 _SIGS = {
     "pdd_version": ([], _int),
+    "pdd_source_digest": ([], ctypes.c_char_p),
+    "pdd_sweep_plan_set_poison": ([_vp, _int], _int),
+    "pdd_sweep_plan_set_segment_bytes": ([_vp, _i64], _int),
     "pdd_last_error": ([], ctypes.c_char_p),
     "pdd_sync": ([_vp], _int),
     "pdd_scratch_release": ([], _int),
@@ -122,6 +120,29 @@ _SIGS = {
 }
 
 
+class PddStaleLibrary(PddLibraryMissing):
+    pass
+
+
+def open_library(path, check=True):
+    """ctypes handle of the libpdd.so at `path` with every signature set.
+    check: the library's compiled-in source digest must equal this tree's
+    (a stale binary is refused, not used)."""
+    h = ctypes.CDLL(path)
+    for name, (argtypes, restype) in _SIGS.items():
+        fn = getattr(h, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
+    if check and _digest.sources_present():
+        got = h.pdd_source_digest().decode()
+        want = _digest.source_digest()
+        if got != want:
+            raise PddStaleLibrary(
+                "%s was built from other sources (digest %s, this tree %s): rebuild it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'`" % (path, got, want))
+    return h
+
+
 def lib():
     """Load (once) and return the ctypes handle of libpdd.so."""
     global _lib
@@ -130,13 +151,13 @@ def lib():
             raise PddLibraryMissing(
                 "libpdd.so not found at %s: build it with "
                 "`python -c 'import __graft_entry__ as g; g.build()'`" % LIB_PATH)
-        h = ctypes.CDLL(LIB_PATH)
-        for name, (argtypes, restype) in _SIGS.items():
-            fn = getattr(h, name)
-            fn.argtypes = argtypes
-            fn.restype = restype
-        _lib = h
+        _lib = open_library(LIB_PATH, check=not _DEV_LIB)
     return _lib
+
+
+def loaded_digest():
+    """Source digest compiled into the loaded library."""
+    return lib().pdd_source_digest().decode()
 
 
 def check(status, what):

@@ -1077,6 +1077,15 @@ extern "C" {
 
 int pdd_version(void) { return 1; }
 
+// PDD_SRC_DIGEST: set by the build (__graft_entry__.build, pypulsar_amd/_digest.py)
+// to the digest of the sources and flags; the marker lets build() read it
+// from the file without loading the library
+#ifndef PDD_SRC_DIGEST
+#define PDD_SRC_DIGEST "unstamped"
+#endif
+static const char kPddDigest[] = "pdd-src-digest:" PDD_SRC_DIGEST;
+const char* pdd_source_digest(void) { return kPddDigest + 15; }
+
 const char* pdd_last_error(void) { return pdd::g_err; }
 
 int pdd_scratch_release(void) {

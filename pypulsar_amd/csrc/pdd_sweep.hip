@@ -342,7 +342,7 @@ __global__ __launch_bounds__(NW * 64) void k_sweep(
       const int cn = c0 + (NBUF - 1) * cc;
       int b = cur + NBUF - 1;
       b = b >= NBUF ? b - NBUF : b;
-      const int n = (cn < C && !(dbg & 1)) ? stage(cn, b) : 0;  // dbg bit 0: timing only
+      const int n = cn < C ? stage(cn, b) : 0;
 #pragma unroll
       for (int s2 = 0; s2 < NBUF - 2; ++s2) pend[s2] = pend[s2 + 1];
       pend[NBUF - 2] = n;
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(NW * 64) void k_sweep(
     const E* img = lds + cur * buf_elems;
 #pragma unroll
     for (int i = 0; i < CC; ++i) {
-      if (i >= ncc || (dbg & 2)) break;  // dbg bit 1: timing only, staging without accumulation
+      if (i >= ncc) break;
       const E* base = img + (int64_t)i * stride + lane;
 #pragma unroll
       for (int j = 0; j < DPW; ++j) {
@@ -903,35 +903,12 @@ __global__ __launch_bounds__(256) void k_fx_patterns_xf(const float* __restrict_
   }
 }
 
-// n DMAs of 64 elements (1 KiB) each, q = first, first + step, ...
-__device__ __forceinline__ int stage_il_dma(uint32_t lds_dst, const float4* src, int ne, int first,
-                                            int step, int lane) {
-  const int nq = (ne + 63) >> 6;
-  for (int q = first; q < nq; q += step) {
-    const float4* s = src + q * 64 + lane;
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %2\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(s), "s"(__builtin_amdgcn_readfirstlane(lds_dst + q * 1024))
-        : "memory");
-  }
-  return first < nq ? (nq - 1 - first) / step + 1 : 0;
-}
-
 // A whole window from ONE wave: runs of up to four consecutive 1 KiB DMAs
 // share one M0 value, the instruction offset (0 / 1024 / 2048 / 3072 bytes)
 // moving both the global source and the LDS destination
 // (scripts/probes/dma_offset.hip checks the LDS side on the device).
-#ifndef PDD_DMA_MODES
-#define PDD_DMA_MODES 0  // dev builds: PDD_SWEEP_DEBUG 512 / 1024 (timing only)
-#endif
 __device__ __forceinline__ int stage_il_dma_win(uint32_t lds_dst, const float4* src, int ne,
-                                                int lane, int nodma = 0) {
+                                                int lane) {
   const int nq = (ne + 63) >> 6;
   uint32_t keep;
 #define PDD_DMA_RUN(TEXT)                                                                      \
@@ -940,11 +917,7 @@ __device__ __forceinline__ int stage_il_dma_win(uint32_t lds_dst, const float4* 
   for (int q = 0; q < nq; q += 4) {
     const float4* s = src + q * 64 + lane;
     const uint32_t m = __builtin_amdgcn_readfirstlane(lds_dst + q * 1024);
-    if (PDD_DMA_MODES && (nodma & 512)) {  // timing only: everything but the DMAs
-      PDD_DMA_RUN("");
-      continue;
-    }
-    switch ((PDD_DMA_MODES && (nodma & 1024)) ? 1 : min(4, nq - q)) {  // (1024, timing only: a run's first DMA)
+    switch (min(4, nq - q)) {
       case 1: PDD_DMA_RUN("global_load_lds_dwordx4 %1, off\n\t"); break;
       case 2: PDD_DMA_RUN("global_load_lds_dwordx4 %1, off\n\t"
                           "global_load_lds_dwordx4 %1, off offset:1024\n\t"); break;
@@ -960,54 +933,14 @@ __device__ __forceinline__ int stage_il_dma_win(uint32_t lds_dst, const float4* 
   }
   return nq;
 }
-#ifndef PDD_IL_DMA_WIN
-#define PDD_IL_DMA_WIN 1
-#endif
 
-// The same from a wave-uniform source address in an SGPR pair (the saddr
-// form; the lanes' VGPR offset is lane * 16 for every DMA): the DMAs take no
-// VALU address arithmetic.  `nq` pieces of 64 elements.
-__device__ __forceinline__ int stage_il_dma_s(uint32_t lds_dst, const float4* src, int nq,
-                                              uint32_t voff, int mode = 0) {
-  // (timing only, 2048: a window's last piece is not staged -- what the
-  // staged bytes cost, not what they are)
-  if (PDD_DMA_MODES && (mode & 2048) && nq > 1) --nq;
-  for (int q = 0; q < nq; q += 4) {
-    const float4* s = src + q * 64;
-    const uint32_t m = __builtin_amdgcn_readfirstlane(lds_dst + q * 1024);
-    uint32_t keep;
-#define PDD_DMA_S(TEXT)                                                                        \
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t" TEXT "s_mov_b32 m0, %0" \
-               : "=&s"(keep) : "v"(voff), "s"(s), "s"(m) : "memory")
-    if (PDD_DMA_MODES && (mode & 512)) {  // timing only: everything but the DMAs
-      PDD_DMA_S("");
-      continue;
-    }
-    switch ((PDD_DMA_MODES && (mode & 1024)) ? 1 : min(4, nq - q)) {  // (1024, timing only: a run's first DMA)
-#ifndef PDD_DMA_POL
-#define PDD_DMA_POL ""  // dev builds: -DPDD_DMA_POL='" nt"' (cache-policy probes)
-#endif
-      case 1: PDD_DMA_S("global_load_lds_dwordx4 %1, %2" PDD_DMA_POL "\n\t"); break;
-      case 2: PDD_DMA_S("global_load_lds_dwordx4 %1, %2" PDD_DMA_POL "\n\t"
-                        "global_load_lds_dwordx4 %1, %2 offset:1024" PDD_DMA_POL "\n\t"); break;
-      case 3: PDD_DMA_S("global_load_lds_dwordx4 %1, %2" PDD_DMA_POL "\n\t"
-                        "global_load_lds_dwordx4 %1, %2 offset:1024" PDD_DMA_POL "\n\t"
-                        "global_load_lds_dwordx4 %1, %2 offset:2048" PDD_DMA_POL "\n\t"); break;
-      default: PDD_DMA_S("global_load_lds_dwordx4 %1, %2" PDD_DMA_POL "\n\t"
-                         "global_load_lds_dwordx4 %1, %2 offset:1024" PDD_DMA_POL "\n\t"
-                         "global_load_lds_dwordx4 %1, %2 offset:2048" PDD_DMA_POL "\n\t"
-                         "global_load_lds_dwordx4 %1, %2 offset:3072" PDD_DMA_POL "\n\t"); break;
-#undef PDD_DMA_S
-    }
-  }
-  return nq;
-}
-
-// The same for a window of nq pieces as ONE asm block per run of up to four:
+// A factorised window of nq pieces from a wave-uniform source address in an
+// SGPR pair (the saddr form; the lanes' VGPR offset is lane * 16 for every
+// DMA: no VALU address arithmetic), as ONE asm block per run of up to four:
 // M0 set once, then the pieces with instruction offsets, each after the
-// first behind an s_cmp / s_cbranch on the remaining count (the compiler's
-// switch over min(4, nq - q) above became a tree of ~20 scalar instructions
-// and four branches per run).  Returns the DMAs issued.
+// first behind an s_cmp / s_cbranch on the remaining count (a compiler switch
+// over min(4, nq - q) became a tree of ~20 scalar instructions and four
+// branches per run).  Returns the DMAs issued.
 __device__ __forceinline__ int stage_il_dma_s2(uint32_t lds_dst, const float4* src, int nq,
                                                uint32_t voff) {
   for (int q = 0; q < nq; q += 4) {
@@ -1041,14 +974,8 @@ __device__ __forceinline__ int stage_il_dma_s2(uint32_t lds_dst, const float4* s
 // Synchronisation of k_sweep_il: one s_barrier per chunk.  Before barrier k
 // the loader waves retire chunk k's DMAs with a counted vmcnt (chunks k+1 ..
 // k+NBUF-2 stay in flight); after it they refill the buffer chunk k-1 used.
-// (An LDS-counter variant without barriers -- loaders publish landed[b],
-// compute waves publish done[b] -- measured slower: the sweep is bound by the
-// L2/MALL->LDS staging rate, ~80 CU-cycles per 1 KiB DMA, not by the barrier.)
-//
-// (Measured and dropped: the compute waves reading their shifts by scalar
-// loads from the global table instead -- SMEM shares lgkmcnt with the LDS
-// reads and returns out of order, so every counted LDS wait became
-// lgkmcnt(0): f32 43 -> 62 ms.)
+// (Measured and dropped, DESIGN.md §3: an LDS-counter hand-off without
+// barriers; the compute waves reading their shifts by scalar loads.)
 // Metadata: mt[dblk][c][ROW], ROW = DB + 4: the tile's DB shifts at channel c
 // relative to their minimum bmin, as byte offsets into the channel's LDS
 // image (16 x elements), then {bmin, span, 0, 0} (in elements).  Loader 0 DMAs
@@ -1057,8 +984,7 @@ __device__ __forceinline__ int stage_il_dma_s2(uint32_t lds_dst, const float4* s
 // vmcnt before barrier k therefore also retires the rows of chunk
 // k + NBUF - 1, which every loader reads after barrier k to issue that
 // chunk's samples, and the compute waves read the shifts of chunk k after
-// the same barrier.  (One ring instead of one per loader: the LDS it frees
-// buys wider chunks -- fewer barriers per channel.)
+// the same barrier.
 __host__ __device__ constexpr int il_ma(int nbuf) { return 2 * nbuf - 2; }
 __host__ __device__ constexpr int il_mr(int nbuf) { return nbuf <= 4 ? 8 : (nbuf <= 8 ? 16 : 32); }
 __host__ __device__ constexpr int il_slot(int cc, int db) { return (cc * (db + 4) + 63) / 64 * 64; }
@@ -1067,25 +993,23 @@ __host__ __device__ constexpr int il_meta_bytes(int nbuf, int cc, int db) {
 }
 
 // Tile order of k_sweep_il.  Blocks b and b+8 share an XCD (and its L2).
-// XCD x owns the time tiles [x*TX, (x+1)*TX), TX = n_tblk / 8, and walks them
-// in 2-D groups of GT time tiles x GJ trial blocks: at one channel the
-// concurrent windows of such a group overlap along both axes (a trial block's
-// window extends its neighbour's by the span, a time tile's by Tq), so the
-// group re-reads each staged element ~GT*GJ*(Tq+S)/(GT*Tq + GJ*S) times from
-// L2.  Leftover time tiles (n_tblk % 8) follow in natural order.
-// dbg bit 4: plain XCD-contiguous order (trial block fastest); bit 5: natural.
+// XCD x walks its time tiles in bands of GT time tiles, each band in 2-D
+// groups of GT time tiles x GJ trial blocks: at one channel the concurrent
+// windows of such a group overlap along both axes (a trial block's window
+// extends its neighbour's by the span, a time tile's by Tq), so the group
+// re-reads each staged element ~GT*GJ*(Tq+S)/(GT*Tq + GJ*S) times from L2.
+// Channel sweeps: XCD x owns the time tiles [x*TX, (x+1)*TX), TX = n_tblk / 8
+// (8 x 4 groups).  Factorised sweeps (XI): band b of XCD x is global band
+// 8b + x, so the eight XCDs sweep eight ADJACENT bands with the same
+// trial-block groups at the same time and the windows two neighbouring bands
+// share are fetched from HBM once, into the Infinity Cache (4 x 2 groups;
+// DESIGN.md §3).  Leftover time tiles (n_tblk % 8) follow in natural order.
 #ifndef PDD_IL_GT
 #define PDD_IL_GT 8
 #endif
 #ifndef PDD_IL_GJ
 #define PDD_IL_GJ 4
 #endif
-// factorised tiles (their own tile-order shape: trial blocks of one time tile
-// share pattern rows, so the shapes are measured separately).  With the
-// XCD-adjacent bands, groups of 4 time tiles x 2 trial blocks: configs[3]
-// stage 2 129.2 -> 120.9 ms per launch, north star 91.9 -> 90.0 (same box,
-// twice each; 8 x 4 / 8 x 2 / 6 x 2 / 4 x 4 / 4 x 1 / 8 x 1 / 2 x 4 / 2 x 2 /
-// 8 x 8 in DESIGN.md §4)
 #ifndef PDD_FX_GT
 #define PDD_FX_GT 4
 #endif
@@ -1093,21 +1017,7 @@ __host__ __device__ constexpr int il_meta_bytes(int nbuf, int cc, int db) {
 #define PDD_FX_GJ 2
 #endif
 template <int GT = PDD_IL_GT, int GJ = PDD_IL_GJ, bool XI = false>
-__device__ __forceinline__ void il_tile_of(int bid, int n_tblk, int n_dblk, int dbg, int& dblk,
-                                           int& tblk) {
-  const int total = n_tblk * n_dblk;
-  if (dbg & 32) {
-    dblk = bid % n_dblk;
-    tblk = bid / n_dblk;
-    return;
-  }
-  if (dbg & 16) {
-    const int full = (total / 8) * 8;
-    const int L = bid >= full ? bid : (bid % 8) * (total / 8) + bid / 8;
-    dblk = L % n_dblk;
-    tblk = L / n_dblk;
-    return;
-  }
+__device__ __forceinline__ void il_tile_of(int bid, int n_tblk, int n_dblk, int& dblk, int& tblk) {
   const int TX = n_tblk / 8;
   const int owned = 8 * TX * n_dblk;
   if (bid >= owned) {
@@ -1126,11 +1036,6 @@ __device__ __forceinline__ void il_tile_of(int bid, int n_tblk, int n_dblk, int 
   r -= jg * gtb * GJ;
   dblk = jg * GJ + r % gj;
   if constexpr (XI) {
-    // the eight XCDs' k-th bands adjacent in time: band b of XCD x is global
-    // band 8b + x (the last, possibly shorter, bands side by side), so the
-    // windows two neighbouring bands share are fetched from HBM once, into
-    // the Infinity Cache, while both XCDs run them (north star 95.4 -> 91.9
-    // ms per launch; configs[3] unchanged, 129.8 / 129.4)
     const int nb = (TX + GT - 1) / GT;
     tblk = (band < nb - 1 ? (band * 8 + x) * GT : 8 * (nb - 1) * GT + x * gtb) + r / gj;
   } else {
@@ -1170,11 +1075,10 @@ __device__ __forceinline__ uint32_t add3_u32(uint32_t a, uint32_t b, uint32_t c)
 // Factorised sweeps (FX): the kernel's "channels" are the channel groups;
 // a chunk's windows (one per pattern its trials use) come from the plan's
 // window records wt[dblk][chunk][kFxWin] = {bmin, length, buffer offset,
-// pattern row | window count << 20}, read by one vector load per loader lane
-// an iteration ahead.
+// pattern row | window count << 20}, one vector load per loader lane, two
+// chunks ahead.
 constexpr int kFxWin = 64;
-template <int G, int DPW, int NCW, int NLW, int CC, int NBUF, bool U16 = false, bool FX = false,
-          int FXS = 0>
+template <int G, int DPW, int NCW, int NLW, int CC, int NBUF, bool U16 = false, bool FX = false>
 __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const float4* __restrict__ R0, int64_t nR, int C, int lo, const int* __restrict__ mt,
     const int* __restrict__ cht, int maxch, float* __restrict__ out, int64_t ld_out, int D,
@@ -1201,93 +1105,51 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   const int per_grp = n_tblk * n_dblk;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const bool stamps = (dbg & 4) != 0;  // dbg bit 2: per-wave cycle stamps into `out`
+  // developer builds only (PDD_SWEEP_DEBUG bit 2): per-wave cycle stamps
+  // written into `out` instead of the plane
+  const bool stamps = (dbg & 4) != 0;
 
   // One tile per workgroup.  (A persistent grid -- 256 workgroups walking
-  // their XCD's tiles in lockstep -- measured no faster: the L2 hit rate of
-  // the staging fell from 77% to 48% at unchanged kernel time, so the staging
-  // is not fabric-bound; and its loop-carried registers spilled.)
-#define IL_TILE_SETUP                                                         \
-  int dblk, tblk;                                                             \
-  const int grp = tile / per_grp;                                             \
-  il_tile_of<FX ? PDD_FX_GT : PDD_IL_GT, FX ? PDD_FX_GJ : PDD_IL_GJ, FX>(           \
-      tile - grp * per_grp, n_tblk, n_dblk, dbg, dblk, tblk);                 \
-  if (PDD_DMA_MODES && (dbg & 384)) tblk = (dbg & 128) ? 0 : (tblk & 7);          \
-  const float4* R = R0 + (int64_t)grp * C * nR;                               \
-  const int64_t t0 = (int64_t)tblk * Tq;                                      \
-  const int* mt_b = mt + ((int64_t)grp * n_dblk + dblk) * (C + 1) * ROW;      \
-  const int* cht_t = cht + ((int64_t)grp * n_dblk + dblk) * (maxch + 1);       \
-  const int nchunk = cht_t[0];                                                \
-  (void)R; (void)t0; (void)mt_b;
-  const int tile = blockIdx.x;
-  IL_TILE_SETUP
-  // FX tiles: the chunk's window records (lane i = window i, one vector
-  // load), and one wave's share of a chunk's window DMAs.  (Measured and
-  // dropped: every wave of the workgroup issuing a share of the DMAs -- the
-  // compute waves' stage-2 work is a quarter of the channel sweep's --
-  // configs[3] 101.6 -> 116.4 ms per launch: the staging does not scale
-  // with the issuing waves.)
+  // their XCD's tiles -- measured no faster for the channel sweep: the L2 hit
+  // rate of the staging fell from 77% to 48% at unchanged kernel time.)
+  int dblk, tblk;
+  const int grp = blockIdx.x / per_grp;
+  il_tile_of<FX ? PDD_FX_GT : PDD_IL_GT, FX ? PDD_FX_GJ : PDD_IL_GJ, FX>(
+      blockIdx.x - grp * per_grp, n_tblk, n_dblk, dblk, tblk);
+  const float4* R = R0 + (int64_t)grp * C * nR;
+  const int64_t t0 = (int64_t)tblk * Tq;
+  const int* mt_b = mt + ((int64_t)grp * n_dblk + dblk) * (C + 1) * ROW;
+  const int* cht_t = cht + ((int64_t)grp * n_dblk + dblk) * (maxch + 1);
+  const int nchunk = cht_t[0];
   const uint32_t img_lds = lds_addr_of(img);
   const uint32_t voff16 = (uint32_t)lane * 16u;
+  // FX tiles: the chunk's window records (lane i = window i, one vector load)
   const int4* wt_b = FX ? wt + ((int64_t)grp * n_dblk + dblk) * maxch * kFxWin : nullptr;
   auto fx_rec = [&](int k) -> int4 {
     if constexpr (FX) return wt_b[(int64_t)min(k, nchunk - 1) * kFxWin + lane];
     else return make_int4(0, 0, 0, 0);
   };
+  // one loader's share of chunk k's window DMAs (windows first, first +
+  // step, ...): lane i computes window i's source, LDS address and piece
+  // count once, then the loader issues its own windows from SGPRs.
+  // (Measured and dropped: every wave of the workgroup issuing a share of
+  // the DMAs -- configs[3] 101.6 -> 116.4 ms per launch.)
   auto fx_issue = [&](int k, const int4& rec, int first, int step) -> int {
     // the compiler's wait for the record (vmcnt(0): it cannot see the DMAs)
     // lands here, before any DMA of this chunk
     asm volatile("" ::"v"(rec.x), "v"(rec.y), "v"(rec.z), "v"(rec.w));
     const int b = k % NBUF;
     const int nw = __builtin_amdgcn_readlane(rec.w, 0) >> 20;
+    const uint64_t sv = (uint64_t)(R + (int64_t)(rec.w & 0xfffff) * nR + (t0 + rec.x - lo));
+    const uint32_t dv = img_lds + (uint32_t)((b * buf_e + rec.z) * 16);
+    const int qv = (rec.y + 63) >> 6;
     int n = 0;
-    if constexpr (FXS & 1) {
-      // lane i = window i: its source, LDS address and piece count in one
-      // pass, then this loader's windows (i = first mod step) from SGPRs
-      int64_t rstride = nR, rrow = rec.w & 0xfffff;
-      // (timing only, wrong results: 8192 -- every window from rows 0..15;
-      // 16384 -- rows 256 elements apart: the address spread of the windows)
-      if (PDD_DMA_MODES && (dbg & 8192)) rrow &= 15;
-      if (PDD_DMA_MODES && (dbg & 16384)) rstride = 256;
-      int64_t toff = t0;
-      // (32768: rows 256 elements apart WITHIN a time tile's own region --
-      // time tile t's windows at ((t mod 256) * 32768 rows) * 256 elements:
-      // the tile's address spread of a time-blocked layout, its data volume)
-      if (PDD_DMA_MODES && (dbg & 32768)) {
-        rstride = 256;
-        toff = (int64_t)((t0 / Tq) % 256) * 32768 * 256;
-      }
-      const uint64_t sv = (uint64_t)(R + rrow * rstride + (toff + rec.x - lo));
-      const uint32_t dv = img_lds + (uint32_t)((b * buf_e + rec.z) * 16);
-      const int qv = (rec.y + 63) >> 6;
-      for (int i = first; i < nw; i += step) {
-        const uint32_t lo32 = __builtin_amdgcn_readlane((uint32_t)sv, i);
-        const uint32_t hi32 = __builtin_amdgcn_readlane((uint32_t)(sv >> 32), i);
-        if constexpr ((FXS & 32) != 0)
-          n += stage_il_dma_s2(__builtin_amdgcn_readlane(dv, i),
-                               (const float4*)(((uint64_t)hi32 << 32) | lo32),
-                               __builtin_amdgcn_readlane(qv, i), voff16);
-        else
-          n += stage_il_dma_s(__builtin_amdgcn_readlane(dv, i),
-                              (const float4*)(((uint64_t)hi32 << 32) | lo32),
-                              __builtin_amdgcn_readlane(qv, i), voff16, dbg & 3584);
-      }
-      return n;
-    }
-    for (int i = 0; i < nw; ++i) {
-      const int bm = __builtin_amdgcn_readlane(rec.x, i);
-      const int len = __builtin_amdgcn_readlane(rec.y, i);
-      const int off = __builtin_amdgcn_readlane(rec.z, i);
-      const int row = __builtin_amdgcn_readlane(rec.w, i) & 0xfffff;
-      if (PDD_IL_DMA_WIN) {
-        // window i from loader i mod NLW, its DMAs in runs sharing M0
-        if (i % step == first)
-          n += stage_il_dma_win(img_lds + (uint32_t)((b * buf_e + off) * 16),
-                                R + (int64_t)row * nR + (t0 + bm - lo), len, lane, dbg & 1536);
-      } else {
-        n += stage_il_dma(img_lds + (uint32_t)((b * buf_e + off) * 16),
-                          R + (int64_t)row * nR + (t0 + bm - lo), len, first, step, lane);
-      }
+    for (int i = first; i < nw; i += step) {
+      const uint32_t lo32 = __builtin_amdgcn_readlane((uint32_t)sv, i);
+      const uint32_t hi32 = __builtin_amdgcn_readlane((uint32_t)(sv >> 32), i);
+      n += stage_il_dma_s2(__builtin_amdgcn_readlane(dv, i),
+                           (const float4*)(((uint64_t)hi32 << 32) | lo32),
+                           __builtin_amdgcn_readlane(qv, i), voff16);
     }
     return n;
   };
@@ -1295,31 +1157,18 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     // ---------------- loader waves: metadata rows + sample windows
     // Top issue priority: a loader shares its SIMD with compute waves that
     // have an LDS read or add ready every cycle.
-    if (!(dbg & 8)) __builtin_amdgcn_s_setprio(3);
+    __builtin_amdgcn_s_setprio(3);
     const int lw = w - NCW;
     int* ring = metar;  // the shared ring (loader 0 fills it)
     // chunk k = channels c0 .. c0 + ncc - 1 (cht: c0 | ncc << 20), packed
     // into its buffer at the per-channel offsets of the metadata rows
     // (loader 0 reads chunk k + MA's table entry one iteration ahead: a
     // scalar load's latency is not on the loaders' per-chunk path)
-    // FXS bit 2 (factorised tiles): the metadata DMAs rotate over the
-    // loaders (chunk k's rows from loader k mod NLW), so loader 0 is not the
-    // one wave with ~5 more DMAs per chunk than the others; each loader reads
-    // its next chunk's table entry one turn (NLW chunks) ahead.
-    constexpr bool kRot = FX && (FXS & 4);
-    const int meta_first = kRot ? MA + ((lw - MA % NLW) % NLW + NLW) % NLW : MA;
-    int e_next = ((kRot || lw == 0) && meta_first < nchunk) ? cht_t[1 + meta_first] : 0;
+    int e_next = (lw == 0 && MA < nchunk) ? cht_t[1 + MA] : 0;
     auto issue_meta = [&](int k) -> int {
-      if (k >= nchunk) return 0;
-      // (timing only, 4096: metadata rows not refreshed after the prologue)
-      if (PDD_DMA_MODES && (dbg & 4096) && k >= MA) return 0;
-      if (kRot ? (k % NLW != lw) : (lw != 0)) return 0;
+      if (k >= nchunk || lw != 0) return 0;
       const int e = k < MA ? cht_t[1 + k] : e_next;
-      if (kRot) {
-        if (k >= MA && k + NLW < nchunk) e_next = cht_t[1 + k + NLW];
-      } else if (k >= MA && k + 1 < nchunk) {
-        e_next = cht_t[2 + k];
-      }
+      if (k >= MA && k + 1 < nchunk) e_next = cht_t[2 + k];
       const int n_int = (e >> 20) * ROW;
       int n = 0;
 #pragma unroll
@@ -1331,35 +1180,25 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       }
       return n;
     };
+    // FX: the records are loaded two chunks ahead; the load issued after a
+    // chunk's DMAs (and the metadata DMAs) is the wave's youngest vector-memory
+    // operation, so the counted wait before the next barrier leaves it in
+    // flight and its latency is off the per-chunk path
     int4 rec_next = fx_rec(0);
-    // FXS 2: the records are loaded two chunks ahead; the load issued after a
-    // chunk's DMAs stays in flight through the wait before the next barrier
-    int4 rec_next2 = (FX && (FXS & 2)) ? fx_rec(1) : make_int4(0, 0, 0, 0);
-    int rec_tail = 0;  // FXS 2: a record load issued after the last chunk's DMAs
+    int4 rec_next2 = fx_rec(1);
+    int rec_tail = 0;  // a record load issued after the last chunk's DMAs
     auto issue_samples = [&](int k) -> int {
-      if (dbg & 1) return 0;
       if constexpr (FX) {
-        // the record of chunk k was loaded an iteration ahead (the wait for
-        // it is the one this iteration already did); load chunk k + 1's now
         const int4 rec = rec_next;
-        if constexpr ((FXS & 2) != 0) {
-          rec_next = rec_next2;  // (chunk k + 2's record: rec_ahead, after the metadata)
-          return fx_issue(k, rec, lw, NLW);
-        }
-        int n = fx_issue(k, rec, lw, NLW);
-        if (k + 1 < nchunk) {
-          rec_next = fx_rec(k + 1);
-          ++n;  // rides on the counted vmcnt
-        }
-        return n;
+        rec_next = rec_next2;  // (chunk k + 2's record: rec_ahead)
+        return fx_issue(k, rec, lw, NLW);
       }
       const int b = k % NBUF;
       // the chunk's window rows {bmin, span, offset, source row} by scalar
       // loads from the global table, all eight issued before one wait: the
       // loaders read no LDS.  (They used to read these fields from the
       // metadata ring, 4 LDS reads per channel queued behind the compute
-      // waves' read stream: configs[3] u8 260.1 -> 239.0 ms per launch,
-      // north star 138.3 -> 121.7, configs[1] u8 25.75 -> 22.33.)
+      // waves' read stream: configs[3] u8 260.1 -> 239.0 ms per launch.)
       static_assert(CC <= 8, "at most eight rows per chunk");
       const int e = cht_t[1 + k];
       const int ncc = e >> 20;
@@ -1369,26 +1208,18 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
 #pragma unroll
       for (int i = 0; i < CC; ++i) {
         if (i >= ncc) break;
-        if (PDD_IL_DMA_WIN) {
-          if (i % NLW == lw)
-            n += stage_il_dma_win(img_lds + (uint32_t)((b * buf_e + rr[i].z) * 16),
-                                  R + (int64_t)(rr[i].w & 0xfffff) * nR + (t0 + rr[i].x - lo),
-                                  Tq + rr[i].y, lane);
-        } else {
-          n += stage_il_dma(img_lds + (uint32_t)((b * buf_e + rr[i].z) * 16),
-                            R + (int64_t)(rr[i].w & 0xfffff) * nR + (t0 + rr[i].x - lo), Tq + rr[i].y,
-                            lw, NLW, lane);
-        }
+        // window i from loader i mod NLW, its DMAs in runs sharing M0
+        if (i % NLW == lw)
+          n += stage_il_dma_win(img_lds + (uint32_t)((b * buf_e + rr[i].z) * 16),
+                                R + (int64_t)(rr[i].w & 0xfffff) * nR + (t0 + rr[i].x - lo),
+                                Tq + rr[i].y, lane);
       }
       return n;
     };
-    // FXS 2: chunk c + 2's record, issued after chunk c's DMAs and the
-    // metadata DMAs (the youngest operation: the wait before the next
-    // barrier leaves it in flight)
     auto rec_ahead = [&](int c) -> int {
       rec_tail = 0;
-      if constexpr (FX && (FXS & 2)) {
-        if (c + 2 < nchunk && !(dbg & 1)) {
+      if constexpr (FX) {
+        if (c + 2 < nchunk) {
           rec_next2 = fx_rec(c + 2);
           rec_tail = 1;
           return 1;
@@ -1413,14 +1244,11 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     for (int k = 0; k < nchunk; ++k) {
       // retire chunk k (and everything older); the NBUF-2 younger chunks stay in flight
       if (stamps) tA = __builtin_amdgcn_s_memtime();
-      int younger = (FX && (FXS & 2)) ? rec_tail : 0;
+      int younger = FX ? rec_tail : 0;
 #pragma unroll
       for (int i = 0; i < NBUF - 2; ++i) younger += hist[i];
       wait_vmcnt(younger);
       if (stamps) { tB = __builtin_amdgcn_s_memtime(); ts_wait += tB - tA; tA = tB; }
-#ifdef PDD_SWEEP_DEV
-      if (!(dbg & 64))  // dbg bit 6 (timing only, wrong results): no chunk barriers
-#endif
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (stamps) { tB = __builtin_amdgcn_s_memtime(); ts_poll += tB - tA; tA = tB; }
@@ -1490,8 +1318,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   static_assert(!U16 || DPW * CC <= 64, "one lane per (channel, trial) shift");
   typedef __attribute__((address_space(3))) u32x4_t lds_u32x4_t;
   uint64_t ts_poll = 0, ts_comp = 0, tA = 0, tB = 0;
-  constexpr bool kPreMeta = FX && (FXS & 8);
-  int vmeta_n = 0, ncc_n = 0;  // kPreMeta: the next chunk's shifts and count
+  int vmeta_n = 0, ncc_n = 0;  // FX: the next chunk's shifts and count
   __builtin_amdgcn_s_barrier();  // prologue barrier (metadata landed)
   asm volatile("" ::: "memory");
   if (stamps) tB = __builtin_amdgcn_s_memtime();
@@ -1501,10 +1328,6 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       tA = __builtin_amdgcn_s_memtime();
       ts_comp += tA - tB;
     }
-
-#ifdef PDD_SWEEP_DEV
-    if (!(dbg & 64))
-#endif
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (stamps) { tB = __builtin_amdgcn_s_memtime(); ts_poll += tB - tA; }
@@ -1526,10 +1349,10 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       return *(const lds_int_t*)(uintptr_t)(lds_addr_of(metar) + (uint32_t)((sl * SLOT + DB + 3) * 4));
     };
     int vmeta, ncc;
-    if constexpr (kPreMeta) {
-      // FXS bit 3: chunk k + 1's shifts and count are read during chunk k (its
-      // ring slot landed before barrier k), so no dependent LDS round trip
-      // stands between a barrier and the first sample read
+    if constexpr (FX) {
+      // chunk k + 1's shifts and count are read during chunk k (its ring
+      // slot landed before barrier k), so no dependent LDS round trip stands
+      // between a barrier and the first sample read
       vmeta = k == 0 ? read_shifts(slot) : vmeta_n;
       ncc = __builtin_amdgcn_readfirstlane(k == 0 ? read_count(slot) : ncc_n) >> 20;
       if (k + 1 < nchunk) {
@@ -1542,79 +1365,72 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       // read -- lanes >= DPW * CC -- measured 1.6% slower for u16, neutral for f32)
       ncc = __builtin_amdgcn_readfirstlane(read_count(slot)) >> 20;
     }
-#ifdef PDD_SWEEP_DEV
-    if (dbg & 64) ncc = cht_t[1 + k] >> 20;  // no barrier: the ring may not hold chunk k yet
-#endif
-    auto chan_base = [&](int) -> uint32_t { return lane_byte + (uint32_t)(b * buf_e * 16); };
-    if (!(dbg & 2)) {
-      if constexpr (U16) {
-        // flush before a chunk could carry a u16 lane past 65535
-        if (since_flush + ncc > flush_n) {
-          since_flush = 0;
-          flush16();
+    const uint32_t cb = lane_byte + (uint32_t)(b * buf_e * 16);
+    if constexpr (U16) {
+      // flush before a chunk could carry a u16 lane past 65535
+      if (since_flush + ncc > flush_n) {
+        since_flush = 0;
+        flush16();
+      }
+      since_flush += ncc;
+      // channel pairs (acc + x_c + x_c+1: one v_add3_u32 per two samples);
+      // u16 chunks always hold an even count (an odd channel count ends in
+      // a pad channel whose window is a row of zeros)
+      u32x4_t v0[G], v1[G];
+      auto pair = [&](int i) {
+#pragma unroll
+        for (int j = 0; j < DPW; ++j) {
+          const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane(vmeta, DPW * i + j);
+          const uint32_t s1 = (uint32_t)__builtin_amdgcn_readlane(vmeta, DPW * (i + 1) + j);
+#pragma unroll
+          for (int g2 = 0; g2 < G; ++g2) {
+            v0[g2] = *(const lds_u32x4_t*)(uintptr_t)(cb + s0 + g2 * 1024);
+            v1[g2] = *(const lds_u32x4_t*)(uintptr_t)(cb + s1 + g2 * 1024);
+          }
+#pragma unroll
+          for (int g2 = 0; g2 < G; ++g2) {
+            a16[j][g2][0] = add3_u32(a16[j][g2][0], v0[g2].x, v1[g2].x);
+            a16[j][g2][1] = add3_u32(a16[j][g2][1], v0[g2].y, v1[g2].y);
+            a16[j][g2][2] = add3_u32(a16[j][g2][2], v0[g2].z, v1[g2].z);
+            a16[j][g2][3] = add3_u32(a16[j][g2][3], v0[g2].w, v1[g2].w);
+          }
+          __builtin_amdgcn_sched_barrier(0);
         }
-        since_flush += ncc;
-        // channel pairs (acc + x_c + x_c+1: one v_add3_u32 per two samples);
-        // u16 chunks always hold an even count (an odd channel count ends in
-        // a pad channel whose window is a row of zeros)
-        u32x4_t v0[G], v1[G];
-        auto pair = [&](int i) {
-          const uint32_t cb = chan_base(i);
+      };
 #pragma unroll
-          for (int j = 0; j < DPW; ++j) {
-            const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane(vmeta, DPW * i + j);
-            const uint32_t s1 = (uint32_t)__builtin_amdgcn_readlane(vmeta, DPW * (i + 1) + j);
+      for (int i = 0; i < CC; i += 2)
+        if (i < ncc) pair(i);
+    } else {
 #pragma unroll
-            for (int g2 = 0; g2 < G; ++g2) {
-              v0[g2] = *(const lds_u32x4_t*)(uintptr_t)(cb + s0 + g2 * 1024);
-              v1[g2] = *(const lds_u32x4_t*)(uintptr_t)(cb + s1 + g2 * 1024);
-            }
+      for (int i = 0; i < CC; ++i) {
+        if (i >= ncc) break;
+        // the channel's DPW read addresses first (readlane + add each), then
+        // two trials of reads in flight: trial j's adds overlap trial j+1's
+        // reads (the accumulators take 64 of the 128 VGPRs, the reads 2 x 4G)
+        uint32_t a[DPW];
 #pragma unroll
-            for (int g2 = 0; g2 < G; ++g2) {
-              a16[j][g2][0] = add3_u32(a16[j][g2][0], v0[g2].x, v1[g2].x);
-              a16[j][g2][1] = add3_u32(a16[j][g2][1], v0[g2].y, v1[g2].y);
-              a16[j][g2][2] = add3_u32(a16[j][g2][2], v0[g2].z, v1[g2].z);
-              a16[j][g2][3] = add3_u32(a16[j][g2][3], v0[g2].w, v1[g2].w);
-            }
-            __builtin_amdgcn_sched_barrier(0);
+        for (int j = 0; j < DPW; ++j)
+          a[j] = cb + (uint32_t)__builtin_amdgcn_readlane(vmeta, DPW * i + j);
+        f32x4_t v[DPW][G];
+#pragma unroll
+        for (int j = 0; j < DPW; ++j)
+#pragma unroll
+          for (int g2 = 0; g2 < G; ++g2)
+            v[j][g2] = *(const lds_f32x4_t*)(uintptr_t)(a[j] + g2 * 1024);
+#pragma unroll
+        for (int j = 0; j < DPW; ++j)
+#pragma unroll
+          for (int g2 = 0; g2 < G; ++g2) {
+            acc[j][g2][0] += v[j][g2].xy;
+            acc[j][g2][1] += v[j][g2].zw;
           }
-        };
+        __builtin_amdgcn_sched_group_barrier(0x002, 2 * DPW, 0);  // addresses
+        __builtin_amdgcn_sched_group_barrier(0x100, G, 0);        // reads, trial 0
+        __builtin_amdgcn_sched_group_barrier(0x100, G, 0);        // reads, trial 1
 #pragma unroll
-        for (int i = 0; i < CC; i += 2)
-          if (i < ncc) pair(i);
-      } else {
-#pragma unroll
-        for (int i = 0; i < CC; ++i) {
-          if (i >= ncc) break;
-          const uint32_t cb = chan_base(i);
-          // the channel's DPW read addresses first (readlane + add each), then
-          // two trials of reads in flight: trial j's adds overlap trial j+1's
-          // reads (the accumulators take 64 of the 128 VGPRs, the reads 2 x 4G)
-          uint32_t a[DPW];
-#pragma unroll
-          for (int j = 0; j < DPW; ++j)
-            a[j] = cb + (uint32_t)__builtin_amdgcn_readlane(vmeta, DPW * i + j);
-          f32x4_t v[DPW][G];
-#pragma unroll
-          for (int j = 0; j < DPW; ++j)
-#pragma unroll
-            for (int g2 = 0; g2 < G; ++g2)
-              v[j][g2] = *(const lds_f32x4_t*)(uintptr_t)(a[j] + g2 * 1024);
-#pragma unroll
-          for (int j = 0; j < DPW; ++j)
-#pragma unroll
-            for (int g2 = 0; g2 < G; ++g2) {
-              acc[j][g2][0] += v[j][g2].xy;
-              acc[j][g2][1] += v[j][g2].zw;
-            }
-          __builtin_amdgcn_sched_group_barrier(0x002, 2 * DPW, 0);  // addresses
-          __builtin_amdgcn_sched_group_barrier(0x100, G, 0);        // reads, trial 0
-          __builtin_amdgcn_sched_group_barrier(0x100, G, 0);        // reads, trial 1
-#pragma unroll
-          for (int j = 0; j < DPW; ++j) {
-            __builtin_amdgcn_sched_group_barrier(0x002, 2 * G, 0);  // adds, trial j
-            if (j + 2 < DPW) __builtin_amdgcn_sched_group_barrier(0x100, G, 0);  // reads, j+2
-          }
+        for (int j = 0; j < DPW; ++j) {
+          __builtin_amdgcn_sched_group_barrier(0x002, 2 * G, 0);  // adds, trial j
+          if (j + 2 < DPW) __builtin_amdgcn_sched_group_barrier(0x100, G, 0);  // reads, j+2
         }
       }
     }
@@ -1678,24 +1494,10 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       }
   }
 }
-#undef IL_TILE_SETUP
-
-// ------------------------------------------------------------------ MFMA sweep (8-bit data)
-// EXPERIMENTAL, developer builds only (-DPDD_SWEEP_DEV, PDD_SWEEP_MX=1):
-// correct (oracle-exact on the variant ladder and the config-3 grid) but
-// measured SLOWER than the u16 VALU kernel on BASELINE configs[3]
-// (28.6 vs 38.1 T adds/s; DESIGN.md §3 "MFMA sweep"): with 16-trial tiles
-// (register-limited: 136 i32 accumulators per wave) it stages 0.11 B of
-// window per add against 0.083 for the 48-trial u16 tiles, and the LDS-DMA
-// staging path (~80-130 CU-cycles per KiB) is what binds both kernels.
-#ifdef PDD_SWEEP_DEV
-#include "dev/sweep_mx_kernel.inc"
-#endif  // PDD_SWEEP_DEV
 
 // ------------------------------------------------------------------ variants
 // kind 0: interleaved image + k_sweep_il (dedicated loader waves, NLW);
-// kind 1: generic striped k_sweep (register staging; sparse-grid fallback);
-// kind 2: 8-bit MFMA sweep k_sweep_mx (NW waves x DPW trials, 16 S times).
+// kind 1: generic striped k_sweep (register staging; sparse-grid fallback).
 struct Variant {
   int kind;
   bool u8;     // kind 1: 8-bit input staged as u16 pairs
@@ -1704,7 +1506,7 @@ struct Variant {
   int threads() const { return (NW + (kind == 0 ? NLW : 0)) * 64; }
   int elem_bytes() const { return kind == 0 ? 16 : (u8 ? 2 * S : 4 * S); }
   int Q() const { return 64 * G; }
-  int TB() const { return kind == 2 ? 16 * S : S * 64 * G; }
+  int TB() const { return S * 64 * G; }
   int DB() const { return NW * DPW; }
   // LDS "stride" (elements per channel per buffer) for a max span
   int64_t stride_for(int max_span) const {
@@ -1725,10 +1527,6 @@ static const Variant kF32Variants[] = {
     {0, false, 4, 4, 4, 8, 8, 2, 2},   // DB 32
     {1, false, 4, 4, 1, 8, 1, 2, 0},   // generic, DB 8
     {1, false, 4, 1, 1, 1, 1, 2, 0}    // generic, DB 1 (any span that fits 160 KB)
-#ifdef PDD_SWEEP_DEV
-    , {0, false, 4, 4, 4, 12, 8, 2, 4}  // dev (PDD_SWEEP_VARIANT=4): 12 + 4 waves, DB 48
-    , {0, false, 4, 4, 4, 10, 8, 2, 6}  // dev (5): 10 + 6 waves, DB 40
-#endif
 };
 // 8-bit input: u16 eighths (12 compute + 4 loader waves: with half the
 // compute per staged byte the extra loaders pay off), then the float32-image
@@ -1741,19 +1539,7 @@ static const Variant kU8Variants[] = {
     {0, false, 4, 4, 4, 8, 8, 2, 2},    // f32 image of u8 data, DB 32
     {1, true, 8, 2, 1, 8, 1, 2, 0},     // generic u16, DB 8
     {1, true, 8, 1, 1, 1, 1, 2, 0}      // generic u16, DB 1
-#ifdef PDD_SWEEP_DEV
-    , {0, false, 8, 2, 4, 12, 8, 3, 4}  // dev (PDD_SWEEP_VARIANT=4): u16 eighths, 3 chunk buffers
-    , {0, false, 8, 2, 4, 10, 8, 2, 6}  // dev (5): 10 compute + 6 loader waves, DB 40
-    , {0, false, 8, 2, 4, 8, 8, 2, 8}   // dev (6): 8 compute + 8 loader waves, DB 32
-#endif
 };
-
-#ifdef PDD_SWEEP_DEV
-// experimental 8-bit MFMA tilings, tried first when PDD_SWEEP_MX=1
-static const Variant kMxVariants[] = {{2, true, 16, 0, 2, 8, 64, 4, 0},
-                                      {2, true, 16, 0, 2, 8, 64, 3, 0},
-                                      {2, true, 16, 0, 2, 8, 64, 2, 0}};
-#endif
 
 // LDS per workgroup: 16-wave (il) tiles run one per CU, <= 8-wave tiles two
 static int64_t lds_budget(const Variant& v) {
@@ -1765,81 +1551,23 @@ static constexpr int kLdsMax = 160 * 1024;
 typedef void (*sweep_il_fn)(const float4*, int64_t, int, int, const int*, const int*, int, float*,
                             int64_t, int, int64_t, int64_t, int64_t, int, int, int, int, int64_t,
                             int64_t, int, float, const float*, int64_t, int64_t, const int4*);
-static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false, int fxs = 0) {
+static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false) {
   if (fx) {
-    // (the staging form is a template parameter: a runtime switch between
-    // the two cost the north star's per-lane form 25%)
+    // factorised stage 2: u16 eighths (8/16-bit input) or float32 quarters
     if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
-      switch (fxs) {
-#ifdef PDD_SWEEP_DEV
-        // the other staging forms, for timing comparisons (PDD_FX_STAGE)
-        case 0: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 0>;
-        case 1: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 1>;
-        case 2: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 2>;
-        case 7: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 7>;
-        case 3: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 3>;
-        case 11: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 11>;
-#endif
-        default: return k_sweep_il<2, 4, 12, 4, 8, 2, true, true, 43>;
-      }
-#ifdef PDD_SWEEP_DEV
-    if (v.S == 8 && v.NW == 10 && v.NLW == 6 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
-      return k_sweep_il<2, 4, 10, 6, 8, 2, true, true, 11>;
-    if (v.S == 8 && v.NW == 8 && v.NLW == 8 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
-      return k_sweep_il<2, 4, 8, 8, 8, 2, true, true, 11>;
-    if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 3)
-      return fxs == 7 ? k_sweep_il<2, 4, 12, 4, 8, 3, true, true, 7>
-                      : k_sweep_il<2, 4, 12, 4, 8, 3, true, true, 3>;
-#endif
-    // float32 quarters (the channel sweep's f32 tiling)
+      return k_sweep_il<2, 4, 12, 4, 8, 2, true, true>;
     if (v.S == 4 && v.NW == 14 && v.NLW == 2 && v.G == 4 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
-      return k_sweep_il<4, 4, 14, 2, 8, 2, false, true, 43>;
-#ifdef PDD_SWEEP_DEV
-    if (v.S == 4 && v.NW == 12 && v.NLW == 4 && v.G == 4 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
-      return k_sweep_il<4, 4, 12, 4, 8, 2, false, true, 43>;
-    if (v.S == 4 && v.NW == 10 && v.NLW == 6 && v.G == 4 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
-      return k_sweep_il<4, 4, 10, 6, 8, 2, false, true, 43>;
-#endif
+      return k_sweep_il<4, 4, 14, 2, 8, 2, false, true>;
     return nullptr;
   }
-#define IL(NCW_, NLW_, CC_, NB_)                                                              \
-  if (v.S == 4 && v.NW == NCW_ && v.NLW == NLW_ && v.CC == CC_ && v.NBUF == NB_ && v.G == 4 && \
-      v.DPW == 4)                                                                               \
-    return k_sweep_il<4, 4, NCW_, NLW_, CC_, NB_>;
-  if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.DPW == 4) {
-    if (v.CC == 8 && v.NBUF == 2) return k_sweep_il<2, 4, 12, 4, 8, 2, true>;
-#ifdef PDD_SWEEP_DEV
-    if (v.CC == 8 && v.NBUF == 3) return k_sweep_il<2, 4, 12, 4, 8, 3, true>;
-  }
-  if (v.S == 8 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2) {
-    if (v.NW == 10 && v.NLW == 6) return k_sweep_il<2, 4, 10, 6, 8, 2, true>;
-    if (v.NW == 8 && v.NLW == 8) return k_sweep_il<2, 4, 8, 8, 8, 2, true>;
-#endif
-  }
-  IL(14, 2, 8, 2)
-#ifdef PDD_SWEEP_DEV
-  IL(12, 4, 8, 2)
-  IL(10, 6, 8, 2)
-#endif
-  IL(8, 2, 8, 2)
-#undef IL
-  return nullptr;
-}
-
-#ifdef PDD_SWEEP_DEV
-typedef void (*sweep_mx_fn)(const uint8_t*, int64_t, int, const uint8_t*, const uint16_t*,
-                            const uint8_t*, int, float*, int64_t, int, int64_t, int64_t, int, int,
-                            int);
-static sweep_mx_fn mx_kernel_for(const Variant& v) {
-  if (v.NW == 8 && v.DPW == 2 && v.S == 16) {
-    if (v.NBUF == 4) return k_sweep_mx<8, 2, 16, 4>;
-    if (v.NBUF == 3) return k_sweep_mx<8, 2, 16, 3>;
-    if (v.NBUF == 2) return k_sweep_mx<8, 2, 16, 2>;
+  if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
+    return k_sweep_il<2, 4, 12, 4, 8, 2, true>;
+  if (v.S == 4 && v.G == 4 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2) {
+    if (v.NW == 14 && v.NLW == 2) return k_sweep_il<4, 4, 14, 2, 8, 2>;
+    if (v.NW == 8 && v.NLW == 2) return k_sweep_il<4, 4, 8, 2, 8, 2>;
   }
   return nullptr;
 }
-
-#endif
 
 typedef void (*sweep_fn)(const void*, int64_t, int, int64_t, const int*, int, int, const int*,
                          const int*, int, const float*, float*, int64_t, int64_t, int, int, int,
@@ -1858,46 +1586,24 @@ static sweep_fn kernel_for(const Variant& v) {
   return nullptr;
 }
 
-// Developer knobs, compiled only into debug builds (-DPDD_SWEEP_DEV): bit 0 of
-// PDD_SWEEP_DEBUG skips re-staging (timing experiments, wrong results), bit 2
-// writes per-wave cycle stamps, bits 4/5 change the tile order;
-// PDD_SWEEP_VARIANT forces a candidate tiling by index.  Production builds
-// ignore the environment.
-static int debug_flags() {
+// Developer knobs, compiled only into developer builds (-DPDD_SWEEP_DEV,
+// scripts/build_dev.sh): PDD_SWEEP_DEBUG bit 2 writes per-wave cycle stamps
+// instead of the plane (scripts/probes/il_stamps.py); PDD_SWEEP_VARIANT
+// forces a candidate tiling by index.  Production builds read no
+// environment variable.
 #ifdef PDD_SWEEP_DEV
+static int debug_flags() {
   const char* e = getenv("PDD_SWEEP_DEBUG");
   return e ? atoi(e) : 0;
-#else
-  return 0;
-#endif
-}
-// Factorised staging form (k_sweep_il's FXS): bit 0 -- the loaders' per-window
-// work from SGPRs (lane i computes window i's addresses once per chunk; each
-// loader walks only its own windows, saddr-form DMAs); bit 1 -- the chunks'
-// window records loaded two chunks ahead (their load latency off the
-// per-chunk barrier path).  Round 4 (dev builds, same box, kernel ms per
-// launch; configs[3] g 4 / north star g 2): 1: 74.0 / 106.9 (round 3), 0:
-// - / 100.8, 2: 86.8 / 111.1, 3: 68.0 / 97.6.  Bit 3 (compute waves read the
-// next chunk's shifts and count during the current chunk): 3 -> 11: 68.4 ->
-// 67.5 / 99.7 -> 98.8.  Bit 5 (a window's DMA runs as one asm block with
-// the piece count tested inside it; the compiler's switch was a tree of ~20
-// scalar instructions and four branches per run): 11 -> 43: 67.2 -> 64.7 /
-// 97.5 -> 94.2 -> 43 for both group sizes.
-static int fx_stage_for(int g) {
-  (void)g;
-#ifdef PDD_SWEEP_DEV
-  if (const char* e = getenv("PDD_FX_STAGE")) return atoi(e);
-#endif
-  return 43;
 }
 static int forced_variant() {
-#ifdef PDD_SWEEP_DEV
   const char* e = getenv("PDD_SWEEP_VARIANT");
   return e ? atoi(e) : -1;
-#else
-  return -1;
-#endif
 }
+#else
+static int debug_flags() { return 0; }
+static int forced_variant() { return -1; }
+#endif
 
 }  // namespace pdd
 
@@ -1911,14 +1617,7 @@ struct pdd_sweep_plan {
   int* d_bspan = nullptr;  // [n_dblk][C]
   int max_bin = 0, min_bin = 0;
   int vi = 0;              // index of the chosen tiling in its candidate list
-  // kind 2 (MFMA) tables: per (trial block, chunk, trial) records, window
-  // starts per (trial block, channel), rows per (trial block, chunk, group)
-  uint8_t* d_meta = nullptr;
-  uint16_t* d_win = nullptr;
-  uint8_t* d_rows = nullptr;
-  int rows_max = 0, nchunk = 0;
   int fx = 0;              // factorised sweep: channels per group (0 = channel by channel)
-  int fx_stage = 0;        // factorised: loaders stage from SGPR window addresses (k_sweep_il)
   int64_t n_pat = 0;       // factorised: pattern series (stage-1 rows, + 1 zero row)
   int64_t fx_rows = 0;     // factorised: metadata rows per trial block (groups + pad groups)
   int fx_rspan = 0;        // factorised: widest relative-shift range of a group (stage-1 LDS)
@@ -1927,6 +1626,8 @@ struct pdd_sweep_plan {
   int* d_gtab = nullptr;   // factorised: per group first pattern + relative-shift range (LDS stage 1)
   int dtype = PDD_F32;     // input element type
   int input_max = 0;       // largest input value (integer input; 0 = the dtype's bound)
+  int poison = 0;          // pdd_sweep_plan_set_poison: 0xFF-fill the pattern image (tests)
+  int64_t seg_bytes = 0;   // pdd_sweep_plan_set_segment_bytes: segment budget cap (0 = default)
   int64_t n_grp = 1;       // independent channel groups (grouped sweep)
   // timing of the sweep kernel (pdd_sweep_set_timing): one event pair per
   // bracketed launch, recorded on the execute stream without host syncs
@@ -1938,10 +1639,6 @@ struct pdd_sweep_plan {
 };
 
 using namespace pdd;
-
-#ifdef PDD_SWEEP_DEV
-#include "dev/sweep_mx_host.inc"
-#endif  // PDD_SWEEP_DEV
 
 // Interleaved path: the output is produced in time segments whose
 // interleaved copy R fits a scratch budget (the library's per-stream
@@ -1970,8 +1667,10 @@ static int64_t il_seg_samples(const pdd_sweep_plan* p, hipStream_t st) {
   // ms per step with 8 launches of 40 GiB; the free-memory cap below keeps
   // smaller or busier GPUs on more, shorter segments)
   if (p->fx) budget = (int64_t)80 << 30;
-  if (const char* e = getenv("PDD_SWEEP_SEG_BYTES")) {
-    budget = std::max<int64_t>(atoll(e), 1 << 16);
+  if (p->seg_bytes > 0) {
+    // a caller's cap (pdd_sweep_plan_set_segment_bytes: tests of the
+    // multi-segment path on small blocks)
+    budget = std::max<int64_t>(p->seg_bytes, 1 << 16);
   } else {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
@@ -1988,6 +1687,7 @@ static int64_t il_seg_samples(const pdd_sweep_plan* p, hipStream_t st) {
 
 struct IlExtra {
   int ds = 1;
+  bool one_seg = false;  // the caller checked that one segment fits (pdd_subband_chain)
   const float* r2_pad = nullptr;
   int64_t r2_nR = 0, r2_ov = 0;
   const float4* R_pre = nullptr;
@@ -2010,7 +1710,8 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
   const int flush_n = std::min(256, 65535 / (vmax * std::max(1, p->fx)));
   const int64_t C = p->C * p->n_grp;  // all channels (groups are contiguous channel ranges)
   const int64_t lo = std::min(0, p->min_bin), hi = std::max(0, p->max_bin);
-  int64_t seg = il_seg_samples(p, as_stream(stream));  // output samples per segment
+  // output samples per segment
+  int64_t seg = ex.one_seg ? std::max<int64_t>(n_out, 1) : il_seg_samples(p, as_stream(stream));
   PDD_REQUIRE(seg > 0, "pdd_sweep_execute: delay span %lld too wide for the segment budget",
               (long long)(hi - lo));
   // equal segments (whole tiles): every launch does the same work
@@ -2098,12 +1799,11 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
                          t_base + lo + x_off, Qs, nR, pad_mode, padvals, R);
     if (hipGetLastError() != hipSuccess) { rc = -3; break; }
     if (p->fx) {
-      // PDD_SWEEP_POISON=1 (a parity-test switch): the pattern rows are filled
-      // with 0xFF bytes first, so a sum that read an element stage 1 did not
-      // write (the per-pattern ranges of fx_build) shows as a NaN / an
-      // overflowed lane instead of a stale-but-plausible value
-      if (getenv("PDD_SWEEP_POISON") && atoi(getenv("PDD_SWEEP_POISON")) &&
-          hipMemsetAsync(P, 0xFF, (size_t)(p->n_pat * nR) * sizeof(uint4), st) != hipSuccess) {
+      // pdd_sweep_plan_set_poison (a parity-test switch): the pattern rows
+      // are filled with 0xFF bytes first, so a sum that read an element stage
+      // 1 did not write (the per-pattern ranges of fx_build) shows as a NaN /
+      // an overflowed lane instead of a stale-but-plausible value
+      if (p->poison && hipMemsetAsync(P, 0xFF, (size_t)(p->n_pat * nR) * sizeof(uint4), st) != hipSuccess) {
         rc = -3;
         break;
       }
@@ -2149,7 +1849,7 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
     const bool bracket = p->timing && p->timed < pdd_sweep_plan::kEvPairs;
     if (p->timing && !bracket) pm->dropped++;
     if (bracket) (void)hipEventRecord(p->ev[2 * p->timed], st);
-    hipLaunchKernelGGL(il_kernel_for(p->v, p->fx != 0, p->fx_stage), dim3((unsigned)blocks), dim3(p->v.threads()),
+    hipLaunchKernelGGL(il_kernel_for(p->v, p->fx != 0), dim3((unsigned)blocks), dim3(p->v.threads()),
                        p->lds_bytes, st, ex.R_pre ? ex.R_pre : (p->fx ? (const float4*)P : R), nR,
                        (int)(p->fx ? p->fx_rows - 1 : p->C), (int)lo, p->d_tab,
                        p->d_bmin, p->maxch, out, ld_out, (int)p->D, Qs, t_base, t_base + cnt,
@@ -2465,14 +2165,6 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
   const int ncand = int_in ? (int)(sizeof(kU8Variants) / sizeof(Variant))
                            : (int)(sizeof(kF32Variants) / sizeof(Variant));
 
-#ifdef PDD_SWEEP_DEV
-  if (dtype == PDD_U8 && n_grp == 1 && getenv("PDD_SWEEP_MX") && atoi(getenv("PDD_SWEEP_MX"))) {
-    for (int mi = 0; mi < 3; ++mi) {
-      const int r = mx_plan_create(host_table, D, C, kMxVariants[mi], 100 + mi, plan_out);
-      if (r <= 0) return r;
-    }
-  }
-#endif
   const int fv = forced_variant();
   for (int vi = (fv >= 0 && fv < ncand) ? fv : 0; vi < ncand; ++vi) {
     const Variant v = cands[vi];
@@ -2644,7 +2336,6 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
       }
       if (fxg) {
         p->fx = fxg;
-        p->fx_stage = fx_stage_for(fxg);
         p->n_pat = T.n_pat;
         p->fx_rows = T.rows_pb;
         p->fx_rspan = T.rspan;  // stage 1 sizes its LDS to it: more workgroups per CU
@@ -2689,7 +2380,7 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
       return -2;
     }
     if (p->lds_bytes > 64 * 1024) {
-      const void* kf = il ? (const void*)il_kernel_for(v, p->fx != 0, p->fx_stage) : (const void*)kernel_for(v);
+      const void* kf = il ? (const void*)il_kernel_for(v, p->fx != 0) : (const void*)kernel_for(v);
       e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, p->lds_bytes);
       if (e != hipSuccess) {
         set_error("pdd_sweep_plan_create: hipFuncSetAttribute: %s", hipGetErrorString(e));
@@ -2747,12 +2438,6 @@ int pdd_sweep_execute_ex(const pdd_sweep_plan* p, const void* x, int64_t N, int6
     while ((1ll << lay.psh) < piece) ++lay.psh;
     lay.pstride = p->C * p->n_grp * piece;
   }
-#ifdef PDD_SWEEP_DEV
-  if (p->v.kind == 2) {
-    PDD_REQUIRE(piece == 0 && x_off == 0, "pdd_sweep_execute: MFMA path reads channel-major input");
-    return execute_mx(p, x, N, ld, pad_mode, padvals, out, ld_out, n_out, stream);
-  }
-#endif
   if (p->v.kind == 0)
     return execute_il(p, x, N, lay, x_off, pad_mode, padvals, out, ld_out, n_out, 0, 1, out_bias,
                       stream);
@@ -2831,24 +2516,38 @@ int pdd_subband_chain(const pdd_sweep_plan* p1, const void* x, int64_t n_raw, in
                   row_g >= 0 && row_d >= 0,
               "pdd_subband_chain: bad shape");
   if (n_out == 0) return 0;
+  // factorised plans sweep single-group input through their pattern image:
+  // they do not chain (pdd.h)
+  if (p1->fx || p2->fx) {
+    set_error("pdd_subband_chain: factorised plans do not chain");
+    return PDD_ENOCHAIN;
+  }
   // stage 1 covers N1 samples in one segment of eighth length Qs1; stage 2
   // reads quarters of length 2 Qs1 (a multiple of its 256-element tile)
   const int64_t Qs1 = cdiv(cdiv(N1, 8), 64 * p1->v.G) * (64 * p1->v.G);
   const int64_t ov = std::max(0, p2->max_bin) + 64;
-  if (!(ov <= Qs1 && (2 * Qs1) % (64 * p2->v.G) == 0 && il_seg_samples(p1, as_stream(stream)) >= N1 &&
-        il_seg_samples(p2, as_stream(stream)) >= n_out)) {
-    set_error("pdd_subband_chain: block of %lld samples does not chain (stage-2 span %d, "
-              "one segment per stage needed)", (long long)N1, p2->max_bin);
+  if (!(ov <= Qs1 && (2 * Qs1) % (64 * p2->v.G) == 0)) {
+    set_error("pdd_subband_chain: block of %lld samples does not chain (stage-2 span %d)",
+              (long long)N1, p2->max_bin);
     return PDD_ENOCHAIN;  // nothing launched: run the stages apart
   }
   const int64_t C2 = p2->C * p2->n_grp;
   const int64_t nR2 = 2 * Qs1 + ov;
-  float4* R2 = nullptr;
   hipStream_t st = as_stream(stream);
-  R2 = static_cast<float4*>(scratch(st, kScratchChain, (size_t)(C2 * nR2) * sizeof(float4)));
+  // stage 2's image first, THEN the one-segment check of both stages (their
+  // budgets are capped by the device memory free after it): the decision is
+  // made once, here, and the stages run with it (IlExtra.one_seg) instead of
+  // re-deriving it from a free-memory figure that their own scratch changes
+  float4* R2 = static_cast<float4*>(scratch(st, kScratchChain, (size_t)(C2 * nR2) * sizeof(float4)));
   if (!R2) return -2;
+  if (!(il_seg_samples(p1, st) >= N1 && il_seg_samples(p2, st) >= n_out)) {
+    set_error("pdd_subband_chain: block of %lld samples does not chain (one segment per stage "
+              "needed)", (long long)N1);
+    return PDD_ENOCHAIN;  // nothing launched: run the stages apart
+  }
   IlExtra e1;
   e1.ds = (int)ds;
+  e1.one_seg = true;
   e1.r2_pad = pad2vals;
   e1.r2_nR = nR2;
   e1.r2_ov = ov;
@@ -2857,6 +2556,7 @@ int pdd_subband_chain(const pdd_sweep_plan* p1, const void* x, int64_t n_raw, in
                       1, p1->n_grp, 0.f, stream, e1);
   if (rc == 0) {
     IlExtra e2;
+    e2.one_seg = true;
     e2.R_pre = R2;
     e2.Qs_pre = 2 * Qs1;
     e2.nR_pre = nR2;
@@ -2873,6 +2573,19 @@ int pdd_sweep_plan_set_input_max(pdd_sweep_plan* p, int max_value) {
   PDD_REQUIRE(max_value >= 1 && max_value <= bound,
               "pdd_sweep_plan_set_input_max: %d outside [1, %d]", max_value, bound);
   p->input_max = max_value;
+  return 0;
+}
+
+int pdd_sweep_plan_set_poison(pdd_sweep_plan* p, int on) {
+  PDD_REQUIRE(p, "pdd_sweep_plan_set_poison: null pointer");
+  p->poison = on ? 1 : 0;
+  return 0;
+}
+
+int pdd_sweep_plan_set_segment_bytes(pdd_sweep_plan* p, int64_t bytes) {
+  PDD_REQUIRE(p, "pdd_sweep_plan_set_segment_bytes: null pointer");
+  PDD_REQUIRE(bytes >= 0, "pdd_sweep_plan_set_segment_bytes: negative budget");
+  p->seg_bytes = bytes;
   return 0;
 }
 
@@ -2924,9 +2637,6 @@ int pdd_sweep_plan_destroy(pdd_sweep_plan* p) {
   if (p->d_pat) (void)hipFree(p->d_pat);
   if (p->d_wt) (void)hipFree(p->d_wt);
   if (p->d_gtab) (void)hipFree(p->d_gtab);
-  if (p->d_meta) (void)hipFree(p->d_meta);
-  if (p->d_win) (void)hipFree(p->d_win);
-  if (p->d_rows) (void)hipFree(p->d_rows);
   delete p;
   return 0;
 }

@@ -49,6 +49,22 @@ def _is_int_pad16(padval):
     return float(padval).is_integer() and 0 <= float(padval) <= 1023
 
 
+# Test switches applied to every sweep plan this process creates (parity
+# tests set them, e.g. with pytest's monkeypatch.setitem; production code
+# never does): poison -- factorised plans fill their pattern image with 0xFF
+# bytes before stage 1 (pdd_sweep_plan_set_poison); segment_bytes > 0 -- the
+# scratch budget of one time segment (pdd_sweep_plan_set_segment_bytes).
+TEST_SWITCHES = {"poison": False, "segment_bytes": 0}
+
+
+def _apply_test_switches(p):
+    if TEST_SWITCHES["poison"]:
+        _lib.check(_lib.lib().pdd_sweep_plan_set_poison(p, 1), "pdd_sweep_plan_set_poison")
+    if TEST_SWITCHES["segment_bytes"]:
+        _lib.check(_lib.lib().pdd_sweep_plan_set_segment_bytes(p, int(TEST_SWITCHES["segment_bytes"])),
+                   "pdd_sweep_plan_set_segment_bytes")
+
+
 class DMSweep(object):
     """A reusable sweep plan: ``DMSweep(dms, freqs, dt)(x)`` -> device plane.
 
@@ -99,10 +115,19 @@ class DMSweep(object):
                 "pdd_sweep_plan_create_ex")
             p = h
             self._plans[code] = p
+            _apply_test_switches(p)
             if self.input_max is not None and code != _lib.F32:
                 _lib.check(_lib.lib().pdd_sweep_plan_set_input_max(p, self.input_max),
                            "pdd_sweep_plan_set_input_max")
         return p
+
+    def set_segment_bytes(self, nbytes, code=None):
+        """Scratch budget of one time segment of this sweep's plans (0 = the
+        library default); tests of the multi-segment path on small blocks."""
+        codes = [code] if code is not None else list(self._plans)
+        for c in codes:
+            _lib.check(_lib.lib().pdd_sweep_plan_set_segment_bytes(self._plan(c), int(nbytes)),
+                       "pdd_sweep_plan_set_segment_bytes")
 
     def info(self, code=_lib.F32):
         a = np.zeros(8, dtype=np.int64)

@@ -58,7 +58,7 @@ def bench_line(log):
 
 
 def main():
-    from pypulsar_amd._lib import source_digest
+    from pypulsar_amd._digest import source_digest
     digest = open(os.path.join(ROOT, "gpurun_out", RUN, "src_digest.txt")).read().strip()
     commit = None
     if source_digest() == digest:
@@ -75,10 +75,16 @@ def main():
         line = bench_line(os.path.join(SRC, "kt_%s.log" % name)) or {}
         plan = line.get("config", {}).get("plan")
         method = line.get("config", {}).get("method")
+        # the run the counters belong to: bench.py reports traffic only for a
+        # line of the same mode, world size and launches per step (columns
+        # per launch)
+        ctx = {"mode": line.get("config", {}).get("mode"), "world": line.get("n_gpus"),
+               "launches_per_step": (line.get("roofline") or {}).get("launches_per_step")}
         fe = per_kernel(os.path.join(SRC, "fe_" + name, "**", "*counter_collection.csv"), "FETCH_SIZE")
         wr = per_kernel(os.path.join(SRC, "wr_" + name, "**", "*counter_collection.csv"), "WRITE_SIZE")
         key = KEYS.get(name, name)
-        stamp = {"round": TAG, "src_digest": digest, "commit": commit, "plan": plan, "method": method}
+        stamp = {"round": TAG, "src_digest": digest, "commit": commit, "plan": plan, "method": method,
+                 "ctx": ctx}
         for n1 in fe:
             if "k_fx_patterns" in n1:
                 pmc[key + "_stage1"] = dict(

@@ -11,7 +11,7 @@ export TMPDIR=/tmp PYTHONDONTWRITEBYTECODE=1
 O=${O:-gpurun_out/ev}
 mkdir -p $O
 PARTS=${PARTS:-"smoke bench prof"}
-timeout -k 10 300 python -c "from pypulsar_amd._lib import source_digest as d; print(d())" > $O/src_digest.txt || exit 1
+timeout -k 10 300 python -c "from pypulsar_amd import _lib; print(_lib.loaded_digest())" > $O/src_digest.txt || exit 1
 echo "digest $(cat $O/src_digest.txt)"
 run() { local t=$1 n=$2; shift 2; timeout -k 10 $t "$@" > $O/$n.json 2> $O/$n.err || { echo "FAIL $n"; tail -5 $O/$n.err; exit 1; }; echo "$n: $(cut -c1-240 $O/$n.json)"; }
 for p in $PARTS; do case $p in

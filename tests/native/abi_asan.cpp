@@ -64,6 +64,8 @@ static void sweep_case(std::mt19937& rng, int64_t C, int64_t N, int64_t D, int s
   CHECK(fx == 0 || ((fx == 2 || fx == 4) && C % fx == 0 && n_pat > 0),
         "factor %d (%lld patterns) for C=%lld dtype=%d", fx, (long long)n_pat, (long long)C, dtype);
   if (fx) ++factorised_cases;
+  // unwritten pattern-image elements would show as NaNs / overflowed lanes
+  CHECK(pdd_sweep_plan_set_poison(plan, 1) == 0, "set_poison");
   int64_t info[8] = {0};
   CHECK(pdd_sweep_plan_info(plan, info) == 0 && info[0] == D && info[1] == C, "plan_info");
   if (timing) CHECK(pdd_sweep_set_timing(plan, 1) == 0, "set_timing");
@@ -234,6 +236,7 @@ int main() {
   int ndev = 0;
   hip_ok(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
   CHECK(pdd_version() >= 1, "version");
+  CHECK(std::strlen(pdd_source_digest()) == 16, "source digest '%s'", pdd_source_digest());
 
   // argument checks: errors come back as status codes with a message
   pdd_sweep_plan* p = nullptr;
@@ -305,6 +308,41 @@ int main() {
     const int rc = pdd_sweep_plan_create_grouped(tab.data(), G, D, C, rep % 2 ? PDD_U8 : PDD_F32, &q);
     CHECK(rc == 0 && q, "grouped create rep %d: %s", rep, pdd_last_error());
     if (q) CHECK(pdd_sweep_plan_destroy(q) == 0, "grouped destroy");
+  }
+  // factorised plans do not chain: pdd_subband_chain says so (PDD_ENOCHAIN)
+  // with nothing launched, instead of failing inside the stages
+  {
+    const int64_t C = 64, D = 48;
+    std::vector<int32_t> tab((size_t)(D * C));
+    for (int64_t d = 0; d < D; ++d)
+      for (int64_t c = 0; c < C; ++c) tab[(size_t)(d * C + c)] = (int32_t)((d * (C - c)) / 16);
+    pdd_sweep_plan *p1 = nullptr, *p2 = nullptr;
+    const int r1 = pdd_sweep_plan_create_ex(tab.data(), D, C, PDD_U8,
+                                            PDD_SWEEP_FACTOR | PDD_SWEEP_FACTOR_FORCE, &p1);
+    std::vector<int32_t> tab2((size_t)(4 * D), 0);
+    for (int64_t d = 0; d < 4; ++d)
+      for (int64_t c = 0; c < D; ++c) tab2[(size_t)(d * D + c)] = (int32_t)(d * (D - c) / 8);
+    const int r2 = pdd_sweep_plan_create_ex(tab2.data(), 4, D, PDD_F32, 0, &p2);
+    CHECK(r1 == 0 && r2 == 0 && pdd_sweep_plan_factor(p1, nullptr) > 0,
+          "chain plans: %d %d %s", r1, r2, pdd_last_error());
+    if (r1 == 0 && r2 == 0) {
+      const int64_t N = 4096;
+      uint8_t* dx = nullptr;
+      float *dpad = nullptr, *dout = nullptr;
+      hip_ok(hipMalloc(&dx, (size_t)(C * N)), "hipMalloc x");
+      hip_ok(hipMalloc(&dpad, (size_t)(D * 4) * 4), "hipMalloc pads");
+      hip_ok(hipMalloc(&dout, (size_t)(4 * N) * 4), "hipMalloc out");
+      hip_ok(hipMemset(dpad, 0, (size_t)(D * 4) * 4), "pads");
+      const int rc = pdd_subband_chain(p1, dx, N, N, 1, PDD_PAD_VALUE, dpad, p2, dpad, dout, N,
+                                       N - 64, 0, 1, nullptr);
+      CHECK(rc == PDD_ENOCHAIN, "factorised stage-1 plan chained: rc %d %s", rc, pdd_last_error());
+      hip_ok(hipDeviceSynchronize(), "sync");
+      hip_ok(hipFree(dx), "free");
+      hip_ok(hipFree(dpad), "free");
+      hip_ok(hipFree(dout), "free");
+    }
+    if (p1) pdd_sweep_plan_destroy(p1);
+    if (p2) pdd_sweep_plan_destroy(p2);
   }
   std::printf("abi_asan: %d sweep cases (%d factorised), %d op cases, %d failures\n", cases,
               factorised_cases, ops, failures);

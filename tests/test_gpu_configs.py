@@ -18,6 +18,8 @@ All inputs are integer-valued 8-bit data with integer pads, so every
 comparison is bit-exact (float32 sums of integers < 2^24), except pad 'mean'
 (1e-5 relative).
 """
+import copy
+
 import numpy as np
 import pytest
 
@@ -133,7 +135,8 @@ def test_northstar_g2_plane(gpu, monkeypatch):
     over groups of 2 channels (the per-lane staging instance of k_sweep_il),
     its plane equals the channel-by-channel kernel bit for bit, and sampled
     rows equal the oracle's per-trial channel sums."""
-    monkeypatch.setenv("PDD_SWEEP_POISON", "1")  # (tests/test_gpu_factor.py)
+    from pypulsar_amd import sweep as _sweep
+    monkeypatch.setitem(_sweep.TEST_SWITCHES, "poison", True)  # (tests/test_gpu_factor.py)
     import torch
     from oracle import spectra_oracle as orc
     from pypulsar_amd import _lib
@@ -166,7 +169,8 @@ def test_config3_timeshard_8_ranks(gpu, monkeypatch):
     overlap) and sweeps the whole 4096-DM grid over its columns with its own
     (factorised) plan; the 8 column blocks concatenate to the one-shot plane
     bit for bit, and sampled rows equal the oracle."""
-    monkeypatch.setenv("PDD_SWEEP_POISON", "1")  # (tests/test_gpu_factor.py)
+    from pypulsar_amd import sweep as _sweep
+    monkeypatch.setitem(_sweep.TEST_SWITCHES, "poison", True)  # (tests/test_gpu_factor.py)
     import torch
     from oracle import spectra_oracle as orc
     from pypulsar_amd.sharding import TimeShardedSweep
@@ -324,6 +328,113 @@ def test_config3_full_length_properties(gpu):
     ps = sub(x8, n_out=n_out)
     assert torch.equal(ps, p8[100:164])
     sub.close()
+
+
+def test_northstar_full_length_g2(gpu, monkeypatch):
+    """The north star at its full size -- 4096 ch x 2^22 samples x 2048 DMs
+    (0-1000, DDplan2b.py:168 grid spacing), 8-bit -- through the bench's own
+    path (DMShardedSweep, one rank, 4 time batches of 2^20 spectra in file
+    order, pieces layout): the planner picks groups of 2 channels, the
+    factorised sweep runs 4 launches (one per batch, ~1.04 M columns each)
+    with its pattern image poisoned before every stage 1, and
+    (a) every plane column equals the channel-by-channel kernel bit for bit
+        (compared in 512-DM chunks);
+    (b) sampled rows equal the independent fused single-DM kernel
+        (Spectra.dedispersed_series: Spectra.dedisperse(dm, trim=True) + the
+        channel sum of bin/waterfaller.py:140, formats/spectra.py:229-260)."""
+    import torch
+    from pypulsar_amd import _lib
+    from pypulsar_amd import sweep as _sweep
+    from pypulsar_amd.formats.spectra import Spectra
+    from pypulsar_amd.sharding import DMShardedSweep, trial_work
+    from pypulsar_amd.sweep import DMSweep
+    monkeypatch.setitem(_sweep.TEST_SWITCHES, "poison", True)
+    C, N, D, NB = 4096, 1 << 22, 2048, 4
+    freqs = band(C)
+    dms = np.linspace(0.0, 1000.0, D)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(23)
+    x_tc = torch.randint(0, 256, (N, C), generator=g, device="cuda", dtype=torch.uint8)
+    ds = DMShardedSweep(dms, freqs, DT, N, dtype=torch.uint8, n_batches=NB,
+                        work=trial_work(dms, 1), device="cuda")
+    assert ds.pieces and ds.n_out == N - 14504 == 4179800
+    g2, n_pat = ds.sw.factor_info(_lib.U8)
+    assert g2 == 2 and n_pat > 0, (g2, n_pat)
+    ds.sw.set_timing(True)
+    planes = ds(x_tc.view(NB, N // NB, C))
+    _, launches = ds.sw.timing_read()
+    ds.sw.set_timing(False)
+    assert launches == NB, launches
+    edges = list(ds.col_edges)
+    n_out = ds.n_out
+    ds.close()
+    del ds
+    torch.cuda.synchronize()
+    _lib.check(_lib.lib().pdd_scratch_release(), "pdd_scratch_release")
+    x8 = x_tc.t().contiguous()
+    del x_tc
+    for lo in range(0, D, 512):
+        ch = DMSweep(dms[lo:lo + 512], freqs, DT, dtype="u8", factor=False)
+        assert ch.factor_info(_lib.U8)[0] == 0
+        pc = ch(x8, n_out=n_out)
+        for k in range(NB):
+            a, b = edges[k], edges[k + 1]
+            assert torch.equal(pc[:, a:b], planes[k][lo:lo + 512]), \
+                "DMs [%d, %d), batch %d: factorised != channel kernel" % (lo, lo + 512, k)
+        ch.close()
+        del pc
+    _lib.check(_lib.lib().pdd_scratch_release(), "pdd_scratch_release")
+    s = Spectra._from_device(freqs, DT, x8.float())
+    del x8
+    for d in (0, 1, 1023, 1024, 2046, 2047):
+        ser = s.dedispersed_series(dms[d], padval=0, trim=True)[:n_out]
+        got = torch.cat([planes[k][d] for k in range(NB)])
+        assert torch.equal(ser, got), "row %d != dedispersed_series" % d
+
+
+def test_config2_subband_benched_size(gpu):
+    """BASELINE configs[2] at the size bench.py --config subband times
+    (4096 ch x 2^20 8-bit samples, DDplan2b -> 64 subbands, res 0.5 ms: 2000
+    DMs at downsamp 4 in 40 passes of 50 DMs, utils/DDplan2b.py:132-168):
+    sampled executor rows equal the two reference steps run on the device
+    through the Spectra API -- Spectra.downsample(4) (spectra.py:329-351),
+    Spectra.subband(64, subDM_k) (spectra.py:96-138) and the dedispersed
+    series of the subbands at each DM of pass k (spectra.py:229-260 +
+    waterfaller.py:140) -- bit for bit (integer data)."""
+    import torch
+    from pypulsar_amd import delays
+    from pypulsar_amd.formats.spectra import Spectra
+    from pypulsar_amd.sweep import DDplanExecutor
+    from pypulsar_amd.utils.ddplan import Observation
+    C, N = 4096, 1 << 20
+    freqs = band(C)
+    plan = Observation(DT, 1400.0, 300.0, C).gen_ddplan(0.0, 1000.0, 64, 0.5)
+    (step,) = plan.DDsteps
+    calls = step.subband_calls()
+    assert (step.downsamp, len(calls), len(calls[0][1])) == (4, 40, 50)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(29)
+    x8 = torch.randint(0, 256, (C, N), generator=g, device="cuda", dtype=torch.uint8)
+    ex = DDplanExecutor(plan, freqs, DT, N, raw8=True)
+    s8 = Spectra(freqs, DT, x8)       # 8-bit data: the Spectra keeps its raw rows
+    (got_step, dms, plane) = ex(s8)[0]
+    del s8
+    ex.close()
+    np.testing.assert_array_equal(dms, step.DMs)
+    n_out = plane.shape[1]
+    _, _, ctr = delays.subband_layout(freqs, 64)
+    assert n_out == N // 4 - int(delays.sweep_table(step.DMs, ctr, DT * 4).max())
+    base = Spectra(freqs, DT, x8)
+    base.downsample(4)
+    for k in (0, 13, 26, 39):
+        subdm, cdms = calls[k]
+        sub = copy.deepcopy(base)
+        sub.subband(64, subdm)
+        np.testing.assert_array_equal(sub.freqs, ctr)
+        for j in (0, 24, 49):
+            ser = sub.dedispersed_series(cdms[j], padval=0, trim=True)[:n_out]
+            assert torch.equal(ser, plane[k * 50 + j]), "pass %d DM %g" % (k, cdms[j])
+        del sub
 
 
 @pytest.mark.parametrize("zdm", ["wrap", "int", "float"])

@@ -17,11 +17,12 @@ DT = 64e-6
 @pytest.fixture(autouse=True)
 def poison_patterns(monkeypatch):
     """Every factorised sweep here first fills its pattern image with 0xFF
-    bytes (PDD_SWEEP_POISON): stage 1 writes only the row elements each
+    bytes (pdd_sweep_plan_set_poison): stage 1 writes only the row elements each
     pattern's trials read (fx_build's per-pattern ranges), so a sum reading
     an unwritten element turns into a NaN / an overflowed lane, not a stale
     value that happens to match."""
-    monkeypatch.setenv("PDD_SWEEP_POISON", "1")
+    from pypulsar_amd import sweep
+    monkeypatch.setitem(sweep.TEST_SWITCHES, "poison", True)
 
 
 @pytest.mark.gpu
@@ -105,9 +106,9 @@ def test_factor_segments_and_column_offsets(gpu, monkeypatch):
     # image rows (channels + patterns + zero rows) x (delay span + ~3000
     # elements of eighths): three or four segments of N
     rows = C + 1 + n_pat + 1
-    monkeypatch.setenv("PDD_SWEEP_SEG_BYTES", str(rows * 16 * (fx.max_bin + 64 + 3000)))
+    fx.set_segment_bytes(rows * 16 * (fx.max_bin + 64 + 3000))
     seg = fx(xd)
-    monkeypatch.delenv("PDD_SWEEP_SEG_BYTES")
+    fx.set_segment_bytes(0)
     assert torch.equal(seg, ref)
     # pieces layout [N/P][C][P] and a column window
     P = 1 << 13

@@ -181,7 +181,8 @@ def test_sweep_ds_factorised(gpu, ds, padval, factor, monkeypatch):
     the raw rows, stage 1 builds the patterns from that image, and the plane
     equals the oracle's Spectra.downsample + per-trial sweep bit for bit.
     factor=True: whatever the planner picks for this grid."""
-    monkeypatch.setenv("PDD_SWEEP_POISON", "1")  # (tests/test_gpu_factor.py)
+    from pypulsar_amd import sweep as _sweep
+    monkeypatch.setitem(_sweep.TEST_SWITCHES, "poison", True)  # (tests/test_gpu_factor.py)
     import torch
     from pypulsar_amd import _lib
     from pypulsar_amd.sweep import DMSweep

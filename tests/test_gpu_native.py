@@ -21,9 +21,8 @@ pytestmark = pytest.mark.gpu
 
 def test_c_abi_driver(gpu):
     assert os.path.exists(DRIVER), "build/abi_driver missing: run __graft_entry__.build()"
-    # (PDD_SWEEP_POISON: unwritten pattern-image elements would show, see
-    # tests/test_gpu_factor.py)
-    r = subprocess.run([DRIVER], capture_output=True, text=True, timeout=180,
-                       env=dict(os.environ, PDD_SWEEP_POISON="1"))
+    # (the driver poisons every factorised plan's pattern image through
+    # pdd_sweep_plan_set_poison, see tests/test_gpu_factor.py)
+    r = subprocess.run([DRIVER], capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "0 failures" in r.stdout
