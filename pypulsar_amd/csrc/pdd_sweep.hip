@@ -696,6 +696,10 @@ __global__ __launch_bounds__(256) void k_fx_patterns(const uint4* __restrict__ R
 // pattern row's elements stage 2 reads (fx_build): kFxE-element blocks
 // outside that range are not written.
 constexpr int kFxE = 512, kFxRspan = 512;
+// float32 stage 1 (k_fx_patterns_xf) builds 1024-element blocks: configs[1]
+// f32 7.31 -> 7.10 ms per launch against 512 (8-bit stage 1: 512 best, 12.5
+// against 14.2 ms at 1024)
+constexpr int kFxEf = 1024;
 // The group's pattern descriptors 64 at a time, one wave-wide load: lane i
 // holds pattern pb + i's relative shifts and row range (fx_build), which the
 // pattern loops take by v_readlane -- no dependent scalar loads per pattern.
@@ -843,10 +847,10 @@ __global__ __launch_bounds__(256) void k_fx_patterns_xf(const float* __restrict_
                                                         float4* __restrict__ P) {
   extern __shared__ __attribute__((aligned(16))) float4 Lf[];
   const int g = blockIdx.x;
-  const int64_t j0 = (int64_t)blockIdx.y * kFxE;
+  const int64_t j0 = (int64_t)blockIdx.y * kFxEf;
   const int p0 = gtab[g], p1 = gtab[g + 1];
   const int lo = gtab[NG + 1 + 2 * g], hi = gtab[NG + 2 + 2 * g];
-  const int W = kFxE + hi - lo;
+  const int W = kFxEf + hi - lo;
   // interior blocks load without per-sample tests (as k_fx_patterns_x)
   const int64_t s_lo = base + j0 + lo, s_hi = s_lo + W - 1 + 3 * Qs;
   const bool inner = j0 + lo >= 0 && j0 + lo + W <= nR && s_lo >= 0 && s_hi < N;
@@ -884,9 +888,9 @@ __global__ __launch_bounds__(256) void k_fx_patterns_xf(const float* __restrict_
       const int4 q = make_int4(0, __builtin_amdgcn_readlane(B.y, i), __builtin_amdgcn_readlane(B.z, i),
                                __builtin_amdgcn_readlane(B.w, i));
       const int64_t jlo = __builtin_amdgcn_readlane(B.lo, i), jhi = nR + __builtin_amdgcn_readlane(B.hi, i);
-      if (j0 >= jhi || j0 + kFxE <= jlo) continue;  // (as k_fx_patterns_lds)
+      if (j0 >= jhi || j0 + kFxEf <= jlo) continue;  // (as k_fx_patterns_lds)
 #pragma unroll
-      for (int e = threadIdx.x; e < kFxE; e += 256) {
+      for (int e = threadIdx.x; e < kFxEf; e += 256) {
         const int64_t j = j0 + e;
         if (j >= nR) break;  // (a block's elements outside [jlo, jhi): written, unread)
         float4 s = Lf[e - lo];
@@ -986,7 +990,9 @@ __device__ __forceinline__ int stage_il_dma_s2(uint32_t lds_dst, const float4* s
 // chunk's samples, and the compute waves read the shifts of chunk k after
 // the same barrier.
 __host__ __device__ constexpr int il_ma(int nbuf) { return 2 * nbuf - 2; }
-__host__ __device__ constexpr int il_mr(int nbuf) { return nbuf <= 4 ? 8 : (nbuf <= 8 ? 16 : 32); }
+// (ring slots: chunk j's rows are written after barrier j - MA, and read up
+// to chunk j's own compute, so MA + 2 slots suffice; 4 for two buffers)
+__host__ __device__ constexpr int il_mr(int nbuf) { return nbuf <= 2 ? 4 : (nbuf <= 4 ? 8 : (nbuf <= 8 ? 16 : 32)); }
 __host__ __device__ constexpr int il_slot(int cc, int db) { return (cc * (db + 4) + 63) / 64 * 64; }
 __host__ __device__ constexpr int il_meta_bytes(int nbuf, int cc, int db) {
   return il_mr(nbuf) * il_slot(cc, db) * 4;
@@ -1095,8 +1101,10 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   constexpr int SLOT = il_slot(CC, DB);
   constexpr int MA = il_ma(NBUF), MR = il_mr(NBUF);
   constexpr int S = U16 ? 8 : 4;  // samples per 16-byte element (quarters / eighths)
-  static_assert(DPW == 4 && G == (U16 ? 2 : 4) && DPW * CC <= 64 && CC % 2 == 0,
-                "4 trials per wave, 4 (f32) or 2 (u16) groups; one lane per (channel, trial)");
+  static_assert((U16 ? (DPW >= 4 && DPW <= 8) : DPW == 4) && G == (U16 ? 2 : 4) &&
+                    DPW * CC <= 64 && CC % 2 == 0,
+                "4 (f32) or 4..8 (u16) trials per wave, 4 (f32) or 2 (u16) groups; one lane "
+                "per (channel, trial)");
   static_assert(NBUF >= 2 && MA >= 2 * NBUF - 2 && MR > MA, "ring geometry");
   extern __shared__ __attribute__((aligned(16))) float smf[];
   uint4* img = reinterpret_cast<uint4*>(smf);
@@ -1271,16 +1279,20 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   }
 
   // ---------------- compute waves: ds_read_b128 at the trial's shift + adds
-  // float32 elements: 4 quarter samples per read, float accumulators.
-  // u16 elements (8-bit data): 8 eighth samples per read as packed u16 pairs,
-  // accumulated with plain 32-bit adds (two u16 lanes per add, no carry while
-  // <= 257 channels of values <= 255 are summed) and flushed to float every
-  // flush_n channels (floor(65535 / the plan's input bound), at most 256) --
-  // exact.
-  // accumulators as float pairs: the adds issue as v_pk_add_f32 (two samples
-  // per VALU instruction: half the issue slots of scalar v_add_f32)
+  // float32 elements: 4 quarter samples per read, float accumulators as float
+  // pairs (the adds issue as v_pk_add_f32: two samples per VALU instruction).
+  // u16 elements (8/16-bit data): 8 eighth samples per read as packed u16
+  // pairs, accumulated with plain 32-bit adds into `lo` (two u16 lanes per
+  // add, one v_add3_u32 per channel pair) and normalised every flush_n
+  // channels: each lane's bit 15 moves into `hi` (a count of 2^15 per lane,
+  // also packed) and `lo` keeps the low 15 bits, so a lane never carries
+  // into its neighbour while flush_n * (input bound) <= 32767 (the plan's
+  // flush_n).  The total hi * 2^15 + lo is exact (float32-exact below 2^24,
+  // the same bound as float accumulators).  16 registers per trial instead
+  // of 24 (u16 partial sums + float totals): the tile holds DPW = 6 trials
+  // per wave (DB 72) in the registers DPW = 4 took.
   typedef float f32x2_t __attribute__((ext_vector_type(2)));
-  constexpr int AJ = DPW, AG = G, AH = S / 2;
+  constexpr int AJ = U16 ? 1 : DPW, AG = U16 ? 1 : G, AH = U16 ? 1 : S / 2;
   f32x2_t acc[AJ][AG][AH];
 #pragma unroll
   for (int j = 0; j < AJ; ++j)
@@ -1288,16 +1300,16 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     for (int g = 0; g < AG; ++g)
 #pragma unroll
       for (int h = 0; h < AH; ++h) acc[j][g][h] = (f32x2_t){0.f, 0.f};
-  uint32_t a16[U16 ? DPW : 1][U16 ? G : 1][4];
+  uint32_t lo16[U16 ? DPW : 1][U16 ? G : 1][4], hi16[U16 ? DPW : 1][U16 ? G : 1][4];
   if constexpr (U16) {
 #pragma unroll
     for (int j = 0; j < DPW; ++j)
 #pragma unroll
       for (int g = 0; g < G; ++g)
 #pragma unroll
-        for (int h = 0; h < 4; ++h) a16[j][g][h] = 0u;
+        for (int h = 0; h < 4; ++h) lo16[j][g][h] = hi16[j][g][h] = 0u;
   }
-  auto flush16 = [&]() {
+  auto normalise16 = [&]() {
     if constexpr (U16) {
 #pragma unroll
       for (int j = 0; j < DPW; ++j)
@@ -1305,9 +1317,19 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
         for (int g = 0; g < G; ++g)
 #pragma unroll
           for (int h = 0; h < 4; ++h) {
-            acc[j][g][h] += (f32x2_t){(float)(a16[j][g][h] & 0xffffu), (float)(a16[j][g][h] >> 16)};
-            a16[j][g][h] = 0u;
+            hi16[j][g][h] += (lo16[j][g][h] >> 15) & 0x00010001u;
+            lo16[j][g][h] &= 0x7fff7fffu;
           }
+    }
+  };
+  // plane value of trial j, group g, eighth / quarter k2 (before out_bias)
+  auto value = [&](int j, int g, int k2) -> float {
+    if constexpr (U16) {
+      const uint32_t l = lo16[j][g][k2 >> 1], h = hi16[j][g][k2 >> 1];
+      return (k2 & 1) ? (float)((h >> 16) * 32768u + (l >> 16))
+                      : (float)((h & 0xffffu) * 32768u + (l & 0xffffu));
+    } else {
+      return acc[j][g][k2 >> 1][k2 & 1];
     }
   };
   int since_flush = 0;
@@ -1367,10 +1389,10 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     }
     const uint32_t cb = lane_byte + (uint32_t)(b * buf_e * 16);
     if constexpr (U16) {
-      // flush before a chunk could carry a u16 lane past 65535
+      // normalise before a chunk could carry a u16 lane past 65535
       if (since_flush + ncc > flush_n) {
         since_flush = 0;
-        flush16();
+        normalise16();
       }
       since_flush += ncc;
       // channel pairs (acc + x_c + x_c+1: one v_add3_u32 per two samples);
@@ -1389,10 +1411,10 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
           }
 #pragma unroll
           for (int g2 = 0; g2 < G; ++g2) {
-            a16[j][g2][0] = add3_u32(a16[j][g2][0], v0[g2].x, v1[g2].x);
-            a16[j][g2][1] = add3_u32(a16[j][g2][1], v0[g2].y, v1[g2].y);
-            a16[j][g2][2] = add3_u32(a16[j][g2][2], v0[g2].z, v1[g2].z);
-            a16[j][g2][3] = add3_u32(a16[j][g2][3], v0[g2].w, v1[g2].w);
+            lo16[j][g2][0] = add3_u32(lo16[j][g2][0], v0[g2].x, v1[g2].x);
+            lo16[j][g2][1] = add3_u32(lo16[j][g2][1], v0[g2].y, v1[g2].y);
+            lo16[j][g2][2] = add3_u32(lo16[j][g2][2], v0[g2].z, v1[g2].z);
+            lo16[j][g2][3] = add3_u32(lo16[j][g2][3], v0[g2].w, v1[g2].w);
           }
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -1435,7 +1457,6 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       }
     }
   }
-  flush16();
   if (stamps) ts_comp += __builtin_amdgcn_s_memtime() - tB;
   if (stamps) {
     if (lane == 0) {
@@ -1470,7 +1491,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
           float x8[8];
 #pragma unroll
           for (int k2 = 0; k2 < 8; ++k2)
-            x8[k2] = (e + k2 * Qs < n_out) ? acc[j][g][k2 >> 1][k2 & 1] + out_bias : pv;
+            x8[k2] = (e + k2 * Qs < n_out) ? value(j, g, k2) + out_bias : pv;
           rrow[e] = make_float4(x8[0], x8[2], x8[4], x8[6]);
           rrow[e + Qs] = make_float4(x8[1], x8[3], x8[5], x8[7]);
           if (e < r2_ov) rrow[2 * Qs + e] = make_float4(x8[2], x8[4], x8[6], pv);
@@ -1490,7 +1511,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       for (int g = 0; g < G; ++g) {
         const int64_t t = t0 + g * 64 + lane;
         if (t < Qs && t_base + t + k2 * Qs < n_out)
-          orow[t + k2 * Qs] = acc[j][g][k2 >> 1][k2 & 1] + out_bias;
+          orow[t + k2 * Qs] = value(j, g, k2) + out_bias;
       }
   }
 }
@@ -1532,13 +1553,17 @@ static const Variant kF32Variants[] = {
 // compute per staged byte the extra loaders pay off), then the float32-image
 // tilings, then the generic u16 kernel.
 static const Variant kU8Variants[] = {
-    {0, false, 8, 2, 4, 12, 8, 2, 4},   // u16 eighths, DB 48, 2 packed buffers of <= 8 channels
-                                        //   (configs[3]: 236.7 ms against 239.0 with 3 buffers,
-                                        //   configs[1] u8 21.4 against 22.3, north star 119.3
-                                        //   against 121.6, once the loaders read no LDS)
+    {0, false, 8, 2, 6, 12, 8, 2, 4},   // u16 eighths, DB 72: 6 trials per compute wave in the
+                                        //   registers 4 took with float totals (k_sweep_il's
+                                        //   15-bit normalised sums), 2 packed buffers
+    {0, false, 8, 2, 4, 12, 8, 2, 4},   // u16 eighths, DB 48 (configs[3]: 236.7 ms against 239.0
+                                        //   with 3 buffers, once the loaders read no LDS)
     {0, false, 4, 4, 4, 8, 8, 2, 2},    // f32 image of u8 data, DB 32
     {1, true, 8, 2, 1, 8, 1, 2, 0},     // generic u16, DB 8
     {1, true, 8, 1, 1, 1, 1, 2, 0}      // generic u16, DB 1
+#ifdef PDD_SWEEP_DEV
+    , {0, false, 8, 2, 5, 12, 8, 2, 4}  // dev (PDD_SWEEP_VARIANT=5): u16 eighths, DB 60
+#endif
 };
 
 // LDS per workgroup: 16-wave (il) tiles run one per CU, <= 8-wave tiles two
@@ -1554,14 +1579,24 @@ typedef void (*sweep_il_fn)(const float4*, int64_t, int, int, const int*, const 
 static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false) {
   if (fx) {
     // factorised stage 2: u16 eighths (8/16-bit input) or float32 quarters
-    if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
-      return k_sweep_il<2, 4, 12, 4, 8, 2, true, true>;
+    if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.CC == 8 && v.NBUF == 2) {
+      if (v.DPW == 6) return k_sweep_il<2, 6, 12, 4, 8, 2, true, true>;
+      if (v.DPW == 4) return k_sweep_il<2, 4, 12, 4, 8, 2, true, true>;
+#ifdef PDD_SWEEP_DEV
+      if (v.DPW == 5) return k_sweep_il<2, 5, 12, 4, 8, 2, true, true>;
+#endif
+    }
     if (v.S == 4 && v.NW == 14 && v.NLW == 2 && v.G == 4 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
       return k_sweep_il<4, 4, 14, 2, 8, 2, false, true>;
     return nullptr;
   }
-  if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
-    return k_sweep_il<2, 4, 12, 4, 8, 2, true>;
+  if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.CC == 8 && v.NBUF == 2) {
+    if (v.DPW == 6) return k_sweep_il<2, 6, 12, 4, 8, 2, true>;
+    if (v.DPW == 4) return k_sweep_il<2, 4, 12, 4, 8, 2, true>;
+#ifdef PDD_SWEEP_DEV
+    if (v.DPW == 5) return k_sweep_il<2, 5, 12, 4, 8, 2, true>;
+#endif
+  }
   if (v.S == 4 && v.G == 4 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2) {
     if (v.NW == 14 && v.NLW == 2) return k_sweep_il<4, 4, 14, 2, 8, 2>;
     if (v.NW == 8 && v.NLW == 2) return k_sweep_il<4, 4, 8, 2, 8, 2>;
@@ -1702,12 +1737,14 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
   const int SP = p->v.S;  // samples per element: 4 (float32 quarters) or 8 (u16 eighths)
   const bool u16 = (SP == 8);
   PDD_REQUIRE(!u16 || p->dtype != PDD_F32, "pdd_sweep_execute: u16 path needs integer input");
-  // packed u16 lanes hold floor(65535 / max value) channel sums: 257 channels
-  // of 8-bit values, 64 of 16-bit values <= 1023, 128 of the wrap-mode
-  // zero-DM image downsampled by 2 (<= 510; pdd_sweep_plan_set_input_max)
+  // packed u16 lanes are normalised to 15 bits every floor(32767 / max value)
+  // channels (k_sweep_il): 128 channels of 8-bit values, 32 of 16-bit values
+  // <= 1023, 64 of the wrap-mode zero-DM image downsampled by 2 (<= 510;
+  // pdd_sweep_plan_set_input_max); factorised plans sum patterns of fx samples
   const int vmax = p->input_max > 0 ? p->input_max : (p->dtype == PDD_U8 ? 255 : 1023);
-  // (factorised: the swept pattern series are sums of fx samples)
-  const int flush_n = std::min(256, 65535 / (vmax * std::max(1, p->fx)));
+  const int flush_n = std::min(256, 32767 / (vmax * std::max(1, p->fx)));
+  PDD_REQUIRE(!u16 || flush_n >= p->v.CC, "pdd_sweep_execute: input bound %d too large for the "
+              "packed 16-bit sums", vmax);
   const int64_t C = p->C * p->n_grp;  // all channels (groups are contiguous channel ranges)
   const int64_t lo = std::min(0, p->min_bin), hi = std::max(0, p->max_bin);
   // output samples per segment
@@ -1812,8 +1849,9 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
         break;
       }
       const int NG = (int)(p->C / p->fx);
-      const dim3 gp((unsigned)NG, (unsigned)cdiv(nR, kFxE));
-      const size_t lds_p = (size_t)(p->fx * (kFxE + p->fx_rspan)) * sizeof(uint4);
+      const int fxe = p->dtype == PDD_F32 ? kFxEf : kFxE;  // stage-1 block length
+      const dim3 gp((unsigned)NG, (unsigned)cdiv(nR, fxe));
+      const size_t lds_p = (size_t)(p->fx * (fxe + p->fx_rspan)) * sizeof(uint4);
       const int64_t b0 = t_base + lo + x_off;
       // (stage-1 kernels are instanced per group size: fx_build makes groups of 2 or 4)
 #define PDD_FX_S1(K2, K4, ...)                                                     \
@@ -2068,12 +2106,13 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
     close();
     rows_pb = std::max(rows_pb, r0);
     // cost model of one tile of this trial block (CU cycles; calibrated on
-    // MI355X for the u16 tiling, BASELINE configs[3] round 3): the channel
-    // sweep's compute waves take ~440 cycles per channel and its loaders
-    // ~1.15 per staged element (LDS-DMA issue), with ~15% synchronisation
-    // (2.06 M cycles per configs[3] tile); the factorised stage 2 has a
-    // quarter of the compute and is loader-bound at ~1.16 x its staging
-    // (1.10 M cycles per configs[3] tile, window DMAs in M0-sharing runs)
+    // MI355X, BASELINE configs[3] and the north star, round 5): the compute
+    // waves take ~440 cycles per channel of a 48-trial u16 tile (~110 per
+    // group of 4 once factorised: the adds and LDS reads scale with C / g and
+    // with the tile's trials), the loaders ~1.0 per staged element (LDS-DMA
+    // issue and landing), and the tile pays the larger of the two plus ~7%
+    // synchronisation.  (Measured, DB 72 per-tile cycles: configs[3] g 4
+    // 1.06 M -- staging-bound --, g 2 1.54 M, north star g 2 1.72 M.)
     int64_t el_b = 0, el_f = 0;  // staged elements: channel sweep / factorised
     for (int64_t c = 0; c < C; ++c) {
       int lo_ = INT32_MAX, hi_ = INT32_MIN;
@@ -2087,13 +2126,15 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
     for (const auto& ch : cw[(size_t)b])
       for (const auto& r : ch) el_f += (r[1] + 63) / 64 * 64;
     if (v.S == 8) {
-      cost_b += 1.15 * std::max(440.0 * (double)C, 1.15 * (double)el_b);
-      cost_f += 1.07 * std::max(110.0 * (double)C, 1.15 * (double)el_f);
+      const double kc = 440.0 * (double)DB / 48.0;  // compute cycles per channel of the tile
+      cost_b += 1.07 * std::max(kc * (double)C, 1.0 * (double)el_b);
+      cost_f += 1.07 * std::max(kc * (double)C / fx, 1.0 * (double)el_f);
     } else {
-      // float32 quarters (configs[1] f32: 1.18 M cycles per tile, compute-bound
-      // at ~1156 cycles per channel; staging alone ~1.28 cycles per element)
-      cost_b += std::max(1156.0 * (double)C, 1.28 * (double)el_b);
-      cost_f += std::max(1156.0 * (double)C / fx, 1.28 * (double)el_f);
+      // float32 quarters (configs[1] f32: 1.18 M cycles per 56-trial tile,
+      // compute-bound at ~1156 cycles per channel; staging ~1.28 per element)
+      const double kc = 1156.0 * (double)DB / 56.0;
+      cost_b += std::max(kc * (double)C, 1.28 * (double)el_b);
+      cost_f += std::max(kc * (double)C / fx, 1.28 * (double)el_f);
     }
   }
   // stage 1 per time tile: every pattern's Tq elements (2 KiB of eighths, 4 KiB
@@ -2358,7 +2399,7 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
               (const void*)k_fx_patterns_xf<4>})
           if (e == hipSuccess && !T.gtab.empty())
             e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)(4 * (kFxE + kFxRspan) * sizeof(uint4)));
+                                    (int)(4 * (kFxEf + kFxRspan) * sizeof(uint4)));
         if (e != hipSuccess) {
           set_error("pdd_sweep_plan_create: %s", hipGetErrorString(e));
           pdd_sweep_plan_destroy(p);

@@ -421,6 +421,7 @@ class TimeShardedSweep(object):
         self.max_bin = int(tab.max()) if tab.size else 0
         self.n_out = self.N - self.max_bin
         assert self.n_out > 0
+        self.align = int(align)
         self.edges = timeshard_edges(self.n_out, self.world, align)
         self.a, self.b = self.edges[self.rank], self.edges[self.rank + 1]
         self.cols = self.b - self.a
@@ -473,10 +474,57 @@ class TimeShardedSweep(object):
             self.full[:, self.edges[r]:self.edges[r + 1]] = self.recv[r]
         return self.full
 
+    def host_step(self, hpart, n_batches=4, copy_stream=None):
+        """The same step from this rank's input in PINNED HOST memory (the
+        PCIe-inclusive form; the filterbank reader fills such
+        a buffer, formats/filterbank.py:143-157): the [n_in, C] spectra are
+        copied H2D in ``n_batches`` chunks on a copy stream, and the plane
+        columns are swept in ``n_batches`` ranges (edges on the 1024-sample
+        tile), range k as soon as the chunks holding its input -- its columns
+        plus the max-delay overlap -- have landed: chunk k+1's copy runs
+        under range k's corner turn and sweep, only chunk 0's is exposed.
+        The plane equals __call__'s bit for bit (every range reads only
+        in-range samples).  Returns this rank's [D, cols] plane."""
+        assert not self.gather, "host_step returns the rank's own plane (no gather)"
+        assert tuple(hpart.shape) == (self.n_in, self.C) and hpart.dtype == self.dtype
+        nb = max(1, min(int(n_batches), max(1, self.cols // self.align)))
+        ce = timeshard_edges(self.cols, nb, self.align)            # column ranges (relative)
+        ie = [0] + [min(self.n_in, ce[k + 1] + self.max_bin) for k in range(nb - 1)] + [self.n_in]
+        if getattr(self, "hx", None) is None:
+            self.hx = torch.empty((self.n_in, self.C), dtype=self.dtype, device=self.device)
+        if self.device.type != "cuda":
+            # (host-only test harness: the same ranges, copies in order)
+            for k in range(nb):
+                self.hx[ie[k]:ie[k + 1]].copy_(hpart[ie[k]:ie[k + 1]])
+                if ie[k + 1] > ie[k]:
+                    self.to_cm(self.hx[ie[k]:ie[k + 1]], self.x[:, ie[k]:ie[k + 1]])
+                a, b = ce[k], ce[k + 1]
+                if b > a:
+                    self.sweep_fn(self.x[:, a:b + self.max_bin], self.out[:, a:b], b - a)
+            return self.out
+        cur = torch.cuda.current_stream(self.device)
+        cs = copy_stream if copy_stream is not None else torch.cuda.Stream(device=self.device)
+        landed = [torch.cuda.Event() for _ in range(nb)]
+        cs.wait_stream(cur)  # the previous step's reads of hx / x are done
+        with torch.cuda.stream(cs):
+            for k in range(nb):
+                if ie[k + 1] > ie[k]:
+                    self.hx[ie[k]:ie[k + 1]].copy_(hpart[ie[k]:ie[k + 1]], non_blocking=True)
+                landed[k].record(cs)
+        for k in range(nb):
+            cur.wait_event(landed[k])
+            if ie[k + 1] > ie[k]:
+                self.to_cm(self.hx[ie[k]:ie[k + 1]], self.x[:, ie[k]:ie[k + 1]])
+            a, b = ce[k], ce[k + 1]
+            if b > a:
+                self.sweep_fn(self.x[:, a:b + self.max_bin], self.out[:, a:b], b - a)
+        return self.out
+
     def close(self):
         if self.sw is not None:
             self.sw.close()
             self.sw = None
+        self.hx = None
 
 
 def split_block(block_tc, n_batches, world, rank):

@@ -7,12 +7,12 @@ import numpy as np
 # (kind, u8, S, G, DPW, NW, CC, NBUF, NLW), as in pdd_sweep.hip
 F32 = [(0, 0, 4, 4, 4, 14, 8, 2, 2), (0, 0, 4, 4, 4, 8, 8, 2, 2),
        (1, 0, 4, 4, 1, 8, 1, 2, 0), (1, 0, 4, 1, 1, 1, 1, 2, 0)]
-U8 = [(0, 0, 8, 2, 4, 12, 8, 2, 4), (0, 0, 4, 4, 4, 8, 8, 2, 2),
+U8 = [(0, 0, 8, 2, 6, 12, 8, 2, 4), (0, 0, 8, 2, 4, 12, 8, 2, 4), (0, 0, 4, 4, 4, 8, 8, 2, 2),
       (1, 1, 8, 2, 1, 8, 1, 2, 0), (1, 1, 8, 1, 1, 1, 1, 2, 0)]
 
 
 def _mr(nbuf):
-    return 8 if nbuf <= 4 else (16 if nbuf <= 8 else 32)
+    return 4 if nbuf <= 2 else (8 if nbuf <= 4 else (16 if nbuf <= 8 else 32))
 
 
 def _slot(cc, db):

@@ -396,7 +396,7 @@ def test_deepcopy_independent(S):
 # plan-selection model tests/plan_model.py (asserted equal to the library's
 # choice): rung i selects candidate i.
 LADDER = {"f32": [2.0, 8.0, 15.0, 40.0],
-          "u8": [1.0, 8.0, 15.0, 40.0]}
+          "u8": [1.0, 3.0, 8.0, 15.0, 40.0]}
 
 
 @pytest.mark.gpu

@@ -291,6 +291,10 @@ def test_timeshard_rehearsal_ranks_concatenate_to_one_shot(world):
         lo, hi = ts.input_range()
         assert hi - lo == ts.cols + int(tab.max()) and hi <= N
         cols.append(ts(block[lo:hi].contiguous()).numpy().copy())
+        # the PCIe-inclusive form (bench.py's end_to_end_pcie leg): the same
+        # columns from chunked copies and column ranges
+        got = ts.host_step(block[lo:hi].contiguous(), n_batches=3).numpy()
+        np.testing.assert_array_equal(got, cols[-1])
     want = orc.sweep_plane(_data(C, N).astype(np.float64), tab)
     np.testing.assert_array_equal(np.concatenate(cols, axis=1).astype(np.float64), want)
 
