@@ -1300,34 +1300,58 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     for (int g = 0; g < AG; ++g)
 #pragma unroll
       for (int h = 0; h < AH; ++h) acc[j][g][h] = (f32x2_t){0.f, 0.f};
-  uint32_t lo16[U16 ? DPW : 1][U16 ? G : 1][4], hi16[U16 ? DPW : 1][U16 ? G : 1][4];
+  // carries: HI8 (DPW > 6) -- one byte per sample, four samples per
+  // register (totals < 255 * 2^15 + 2^16, checked by the plan: 12 registers
+  // per trial, DPW = 8 fits); else one u16 per sample, two per register
+  // (totals < 2^24: 16 registers per trial)
+  constexpr bool HI8 = U16 && DPW > 6;
+  constexpr int NHI = U16 ? (HI8 ? 2 : 4) : 1;
+  uint32_t lo16[U16 ? DPW : 1][U16 ? G : 1][4], hic[U16 ? DPW : 1][U16 ? G : 1][NHI];
   if constexpr (U16) {
 #pragma unroll
     for (int j = 0; j < DPW; ++j)
 #pragma unroll
-      for (int g = 0; g < G; ++g)
+      for (int g = 0; g < G; ++g) {
 #pragma unroll
-        for (int h = 0; h < 4; ++h) lo16[j][g][h] = hi16[j][g][h] = 0u;
+        for (int h = 0; h < 4; ++h) lo16[j][g][h] = 0u;
+#pragma unroll
+        for (int h = 0; h < NHI; ++h) hic[j][g][h] = 0u;
+      }
   }
   auto normalise16 = [&]() {
     if constexpr (U16) {
 #pragma unroll
       for (int j = 0; j < DPW; ++j)
 #pragma unroll
-        for (int g = 0; g < G; ++g)
+        for (int g = 0; g < G; ++g) {
+          if constexpr (HI8) {
+            // lo words 2q and 2q + 1 -> carry bytes 0 / 2 and 1 / 3 of hic[q]
 #pragma unroll
-          for (int h = 0; h < 4; ++h) {
-            hi16[j][g][h] += (lo16[j][g][h] >> 15) & 0x00010001u;
-            lo16[j][g][h] &= 0x7fff7fffu;
+            for (int q = 0; q < 2; ++q) {
+              const uint32_t ca = (lo16[j][g][2 * q] >> 15) & 0x00010001u;
+              const uint32_t cb = (lo16[j][g][2 * q + 1] >> 15) & 0x00010001u;
+              hic[j][g][q] += ca + (cb << 8);
+            }
+          } else {
+#pragma unroll
+            for (int h = 0; h < 4; ++h) hic[j][g][h] += (lo16[j][g][h] >> 15) & 0x00010001u;
           }
+#pragma unroll
+          for (int h = 0; h < 4; ++h) lo16[j][g][h] &= 0x7fff7fffu;
+        }
     }
   };
   // plane value of trial j, group g, eighth / quarter k2 (before out_bias)
   auto value = [&](int j, int g, int k2) -> float {
     if constexpr (U16) {
-      const uint32_t l = lo16[j][g][k2 >> 1], h = hi16[j][g][k2 >> 1];
-      return (k2 & 1) ? (float)((h >> 16) * 32768u + (l >> 16))
-                      : (float)((h & 0xffffu) * 32768u + (l & 0xffffu));
+      const int h = k2 >> 1, half = k2 & 1;
+      const uint32_t l = half ? (lo16[j][g][h] >> 16) : (lo16[j][g][h] & 0xffffu);
+      uint32_t c;
+      if constexpr (HI8)
+        c = (hic[j][g][h >> 1] >> (8 * ((h & 1) + 2 * half))) & 0xffu;
+      else
+        c = half ? (hic[j][g][h] >> 16) : (hic[j][g][h] & 0xffffu);
+      return (float)(c * 32768u + l);
     } else {
       return acc[j][g][k2 >> 1][k2 & 1];
     }
@@ -1552,6 +1576,13 @@ static const Variant kF32Variants[] = {
 // 8-bit input: u16 eighths (12 compute + 4 loader waves: with half the
 // compute per staged byte the extra loaders pay off), then the float32-image
 // tilings, then the generic u16 kernel.
+// Factorised 8/16-bit plans try these first (before their channel tiling):
+// u16 eighths, DB 96 -- 8 trials per compute wave with byte-wide carry
+// counts (plane sums < 255 * 2^15: C * input bound checked by the plan).
+// configs[3] g 4 101.8 -> 97.2 ms per launch, north star g 2 83.3 -> 81.6
+// against DB 72; the channel kernel is 2% slower at DB 96 (configs[1] u8
+// 21.0 -> 21.5 ms), so channel plans keep DB 72.
+static const Variant kU8FxVariants[] = {{0, false, 8, 2, 8, 12, 8, 2, 4}};
 static const Variant kU8Variants[] = {
     {0, false, 8, 2, 6, 12, 8, 2, 4},   // u16 eighths, DB 72: 6 trials per compute wave in the
                                         //   registers 4 took with float totals (k_sweep_il's
@@ -1580,6 +1611,7 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false) {
   if (fx) {
     // factorised stage 2: u16 eighths (8/16-bit input) or float32 quarters
     if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.CC == 8 && v.NBUF == 2) {
+      if (v.DPW == 8) return k_sweep_il<2, 8, 12, 4, 8, 2, true, true>;
       if (v.DPW == 6) return k_sweep_il<2, 6, 12, 4, 8, 2, true, true>;
       if (v.DPW == 4) return k_sweep_il<2, 4, 12, 4, 8, 2, true, true>;
 #ifdef PDD_SWEEP_DEV
@@ -2362,17 +2394,39 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
       // 8/16-bit single-group sweeps: the factorised tables when they pay
       // groups of 4 channels, or of 2 where 4 do not fit or pay (the
       // cheaper by the cost model; PDD_SWEEP_FACTOR_G2 / _G4: that size only)
+      // Factorised u16 plans first try their own 96-trial tiling
+      // (kU8FxVariants: measured faster for factorised stage 2, slower for
+      // the channel kernel), then the channel plan's tiling.
       FxTables T, T2;
       const bool force = (flags & PDD_SWEEP_FACTOR_FORCE) != 0;
       int fxg = 0;
       if ((flags & PDD_SWEEP_FACTOR) && n_grp == 1 && v.S == (dtype == PDD_F32 ? 4 : 8) &&
           il_kernel_for(v, true)) {
-        if (!(flags & PDD_SWEEP_FACTOR_G2) && fx_build(host_table, D, C, v, buf_e, 4, force, T))
-          fxg = 4;
-        if (!(flags & PDD_SWEEP_FACTOR_G4) && fx_build(host_table, D, C, v, buf_e, 2, force, T2) &&
-            (fxg == 0 || T2.cost_f < T.cost_f)) {
-          fxg = 2;
-          std::swap(T, T2);
+        std::vector<Variant> fc;
+        if (v.S == 8)
+          for (const Variant& x : kU8FxVariants)
+            if (C * (dtype == PDD_U8 ? 255 : 1023) <= 255 * 32768 && il_kernel_for(x, true))
+              fc.push_back(x);
+        fc.push_back(v);
+        for (const Variant& f : fc) {
+          const int64_t room_f = lds_budget(f) - il_meta_bytes(f.NBUF, f.CC, f.DB());
+          const int64_t buf_f = std::max<int64_t>(0, room_f / (f.NBUF * 16) / 64 * 64);
+          if (!(flags & PDD_SWEEP_FACTOR_G2) && fx_build(host_table, D, C, f, buf_f, 4, force, T))
+            fxg = 4;
+          if (!(flags & PDD_SWEEP_FACTOR_G4) && fx_build(host_table, D, C, f, buf_f, 2, force, T2) &&
+              (fxg == 0 || T2.cost_f < T.cost_f)) {
+            fxg = 2;
+            std::swap(T, T2);
+          }
+          if (fxg) {
+            // the plan runs the factorised tiling: its trial blocks, LDS
+            p->v = f;
+            p->n_dblk = cdiv(D, f.DB());
+            p->Dpad = p->n_dblk * f.DB();
+            p->stride = (int)buf_f;
+            p->lds_bytes = (int)(f.NBUF * buf_f * 16 + il_meta_bytes(f.NBUF, f.CC, f.DB()));
+            break;
+          }
         }
       }
       if (fxg) {
@@ -2421,7 +2475,7 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
       return -2;
     }
     if (p->lds_bytes > 64 * 1024) {
-      const void* kf = il ? (const void*)il_kernel_for(v, p->fx != 0) : (const void*)kernel_for(v);
+      const void* kf = il ? (const void*)il_kernel_for(p->v, p->fx != 0) : (const void*)kernel_for(v);
       e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, p->lds_bytes);
       if (e != hipSuccess) {
         set_error("pdd_sweep_plan_create: hipFuncSetAttribute: %s", hipGetErrorString(e));
