@@ -1255,6 +1255,7 @@ def subband_bench(args, cfg, rank, world, dev):
     if world > 1:
         el = max_over_ranks(el, dev)
     ms = el / args.steps * 1e3
+    roof = subband_roofline(ex, s, one, args.steps, C, N) if world == 1 else None
     line = {
         "metric": "DM-trial samples*channels/sec (node) + % HBM roofline",
         "value": units * args.steps * world / el,
@@ -1271,10 +1272,66 @@ def subband_bench(args, cfg, rank, world, dev):
                    "config_name": "subband", "channels": C, "samples": N,
                    "dm_trials": int(sum(len(st.DMs) for st in plan.DDsteps)),
                    "parallelism": "tb%d" % world},
-        "roofline": None,
+        "roofline": roof,
         "cpu_baseline": None,
     }
     _finish(args, world, line)
+
+
+def subband_roofline(ex, spectra, one, steps, C, N):
+    """Per-stage HBM roofline of a chained two-stage DDplan step (configs[2]:
+    pdd_subband_chain = the stage-1 interleave pre-pass (8-bit rows co-added
+    by ds into u16 eighths), the stage-1 grouped sweep writing stage 2's
+    float32 quarters image, the stage-2 grouped sweep writing the plane).
+    The two sweep kernels are timed by their plans' HIP event pairs, the
+    whole chain by events around it on the same stream; the pre-pass is the
+    remainder.  Algorithmic bytes per stage: its input once + its output
+    once."""
+    st = [s for s in ex.steps if s.two_stage and s.chain]
+    if len(ex.steps) != 1 or not st:
+        return None
+    s = st[0]
+    i1, i2 = s.g1.info(), s.g2.info()
+    n1 = N // s.ds
+    tq = i1["samples_per_block"] // 8                   # u16 eighths: Tq elements
+    qs1 = -(-(-(-n1 // 8)) // tq) * tq
+    nr1 = qs1 + max(0, i1["max_bin"]) - min(0, i1["min_bin"]) + 64
+    rows2 = s.ncall * s.nsub
+    nr2 = 2 * qs1 + max(0, i2["max_bin"]) + 64
+    b_pre = C * N + C * nr1 * 16                         # raw 8-bit rows in, u16 eighths out
+    b_s1 = C * nr1 * 16 + rows2 * nr2 * 16               # eighths in, quarters image out
+    b_s2 = rows2 * nr2 * 16 + s.ncall * s.per * s.n_out * 4   # quarters in, plane out
+    s.g1.set_timing(True)
+    s.g2.set_timing(True)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(steps):
+        one()
+    e1.record()
+    torch.cuda.synchronize()
+    t_all = e0.elapsed_time(e1) / steps
+    k1, l1 = s.g1.timing_read()
+    k2, l2 = s.g2.timing_read()
+    s.g1.set_timing(False)
+    s.g2.set_timing(False)
+    k1, k2 = k1 / steps, k2 / steps
+    pre = max(t_all - k1 - k2, 1e-6)
+    stages = []
+    for name, b, t in (("k_interleave_u16_ds_v (stage-1 pre-pass: co-add + eighths)", b_pre, pre),
+                       ("k_sweep_il u16 grouped, stage 1 -> stage-2 quarters image", b_s1, k1),
+                       ("k_sweep_il f32 grouped, stage 2 -> plane", b_s2, k2)):
+        gbs = b / (t * 1e-3) / 1e9
+        stages.append({"kernel": name, "ms": t, "bytes": b, "achieved_GBs": gbs,
+                       "frac": gbs / PEAK_HBM_GBS})
+    tot = b_pre + b_s1 + b_s2
+    return {"bound": "hbm", "achieved": tot / (t_all * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
+            "unit": "GB/s", "frac": tot / (t_all * 1e-3) / 1e9 / PEAK_HBM_GBS, "traffic": None,
+            "stages": stages, "launches": [l1 // steps, l2 // steps],
+            "note": "per-stage algorithmic bytes (each stage's input once + output once) over "
+                    "its own time: the sweeps by their HIP event pairs, the pre-pass as the "
+                    "remainder of the chain's events; the stage-1 sweep's adds per byte make it "
+                    "LDS-bound rather than HBM-bound (DESIGN.md §4)"}
 
 
 if __name__ == "__main__":

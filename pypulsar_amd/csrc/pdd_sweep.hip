@@ -426,22 +426,30 @@ __device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
   return (uint32_t)(uintptr_t)(const lds_float_t*)p;
 }
 
-// 64 consecutive ints -> LDS by one LDS-DMA wave-instruction (lane l loads
-// src + min(l, n - 1)); used for the per-chunk metadata so it travels on the
-// same counted vmcnt as the sample DMAs and never touches a VGPR early.
-__device__ __forceinline__ void dma_ints(int* lds_dst, const int* src, int n, int lane) {
-  const int* p = src + min(lane, n - 1);
-  const uint32_t la = lds_addr_of(lds_dst);
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dword %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(p), "s"(__builtin_amdgcn_readfirstlane(la))
-      : "memory");
+// 256 consecutive ints (1 KiB) -> LDS by one dwordx4 LDS-DMA
+// wave-instruction (lane l: ints 4l .. 4l + 3); lanes past n (a multiple of
+// 4) stay idle, so nothing lands past the n ints; src and lds_dst 16-B
+// aligned.  Used for the per-chunk metadata rows, so they travel on the same
+// counted vmcnt as the sample DMAs and never touch a VGPR early.  (Measured
+// and dropped, round 5: the rows one chunk further ahead, kept in flight
+// through the next barrier by the compiler's LDS-DMA builtin -- the
+// staging-free skeleton 48 -> 32 ms per configs[3] launch, but production
+// 102.2 -> 107.1 ms.)
+__device__ __forceinline__ void dma_ints4(int* lds_dst, const int* src, int n, int lane) {
+  const uint32_t la = __builtin_amdgcn_readfirstlane(lds_addr_of(lds_dst));
+  if (lane * 4 < n) {
+    const int* p = src + lane * 4;
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(p), "s"(la)
+        : "memory");
+  }
 }
 
 
@@ -1100,6 +1108,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   constexpr int ROW = DB + 4;
   constexpr int SLOT = il_slot(CC, DB);
   constexpr int MA = il_ma(NBUF), MR = il_mr(NBUF);
+  static_assert(ROW % 4 == 0, "metadata rows land as 16-byte quads");
   constexpr int S = U16 ? 8 : 4;  // samples per 16-byte element (quarters / eighths)
   static_assert((U16 ? (DPW >= 4 && DPW <= 8) : DPW == 4) && G == (U16 ? 2 : 4) &&
                     DPW * CC <= 64 && CC % 2 == 0,
@@ -1179,11 +1188,14 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       if (k >= MA && k + 1 < nchunk) e_next = cht_t[2 + k];
       const int n_int = (e >> 20) * ROW;
       int n = 0;
+      // 1 KiB per DMA: a chunk's rows in ceil(n_int / 256) instructions (the
+      // metadata DMAs of a 96-trial chunk: 4 instead of 13 dword DMAs;
+      // configs[3] stage 2 103.1 -> 102.2 ms per launch)
 #pragma unroll
-      for (int m = 0; m < SLOT / 64; ++m) {
-        if (m * 64 >= n_int) break;
-        dma_ints(ring + (k % MR) * SLOT + m * 64, mt_b + (int64_t)(e & 0xfffff) * ROW + m * 64,
-                 n_int - m * 64, lane);
+      for (int m = 0; m < (SLOT + 255) / 256; ++m) {
+        if (m * 256 >= n_int) break;
+        dma_ints4(ring + (k % MR) * SLOT + m * 256, mt_b + (int64_t)(e & 0xfffff) * ROW + m * 256,
+                  n_int - m * 256, lane);
         ++n;
       }
       return n;
@@ -1196,6 +1208,9 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     int4 rec_next2 = fx_rec(1);
     int rec_tail = 0;  // a record load issued after the last chunk's DMAs
     auto issue_samples = [&](int k) -> int {
+#ifdef PDD_SWEEP_DEV
+      if (dbg & 1) return 0;  // (developer builds, timing only: no window staging)
+#endif
       if constexpr (FX) {
         const int4 rec = rec_next;
         rec_next = rec_next2;  // (chunk k + 2's record: rec_ahead)
@@ -1412,6 +1427,9 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       ncc = __builtin_amdgcn_readfirstlane(read_count(slot)) >> 20;
     }
     const uint32_t cb = lane_byte + (uint32_t)(b * buf_e * 16);
+#ifdef PDD_SWEEP_DEV
+    if (dbg & 2) continue;  // (developer builds, timing only: no reads / adds)
+#endif
     if constexpr (U16) {
       // normalise before a chunk could carry a u16 lane past 65535
       if (since_flush + ncc > flush_n) {
@@ -1655,7 +1673,10 @@ static sweep_fn kernel_for(const Variant& v) {
 
 // Developer knobs, compiled only into developer builds (-DPDD_SWEEP_DEV,
 // scripts/build_dev.sh): PDD_SWEEP_DEBUG bit 2 writes per-wave cycle stamps
-// instead of the plane (scripts/probes/il_stamps.py); PDD_SWEEP_VARIANT
+// instead of the plane (scripts/probes/il_stamps.py); bits 0 / 1 (timing
+// only, wrong planes) drop the loaders' window DMAs / the compute waves'
+// reads and adds (k_sweep_il), the time decomposition of DESIGN.md §3;
+// PDD_SWEEP_VARIANT
 // forces a candidate tiling by index.  Production builds read no
 // environment variable.
 #ifdef PDD_SWEEP_DEV

@@ -360,6 +360,28 @@ class GroupedSweep(object):
              ptr(padvals), ptr(out), out.stride(0), n_out, row_g, row_d, stream_ptr(stream))
         return out
 
+    def info(self):
+        """Plan extents (pdd_sweep_plan_info) as a dict (DMs per block, ...)."""
+        a = np.zeros(8, dtype=np.int64)
+        _lib.check(_lib.lib().pdd_sweep_plan_info(self._plan, a.ctypes.data_as(ctypes.c_void_p)),
+                   "pdd_sweep_plan_info")
+        keys = ("D", "C", "dms_per_block", "samples_per_block", "lds_bytes", "max_bin", "min_bin",
+                "variant")
+        return dict(zip(keys, (int(v) for v in a)))
+
+    def set_timing(self, on=True):
+        """Bracket every sweep-kernel launch of this plan with a HIP event pair."""
+        _lib.check(_lib.lib().pdd_sweep_set_timing(self._plan, int(bool(on))),
+                   "pdd_sweep_set_timing")
+
+    def timing_read(self):
+        """(summed kernel ms, launches) since set_timing / the last read."""
+        v = ctypes.c_float(0.0)
+        n = ctypes.c_int64(0)
+        _lib.check(_lib.lib().pdd_sweep_timing_read(self._plan, ctypes.byref(v), ctypes.byref(n)),
+                   "pdd_sweep_timing_read")
+        return float(v.value), int(n.value)
+
     def execute_ds(self, x8, ds, n_out, out, row_g, row_d, pad_mode=_lib.PAD_VALUE, padvals=None,
                    stream=None):
         """The grouped sweep of ``x8`` ([n_grp*C, n_raw] uint8) downsampled by
