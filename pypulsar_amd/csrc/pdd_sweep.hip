@@ -1074,8 +1074,11 @@ __device__ __forceinline__ il_rows8 il_load_rows8(const int* p) {
       "s_load_dwordx4 %4, %8, %13\n\ts_load_dwordx4 %5, %8, %14\n\t"
       "s_load_dwordx4 %6, %8, %15\n\ts_load_dwordx4 %7, %8, %16\n\t"
       "s_waitcnt lgkmcnt(0)"
-      : "=s"(o.r0), "=s"(o.r1), "=s"(o.r2), "=s"(o.r3), "=s"(o.r4), "=s"(o.r5), "=s"(o.r6),
-        "=s"(o.r7)
+      // early-clobber outputs: a row's registers must not overlap the base
+      // address the later loads of the block still read (a load returning
+      // before the next one issues would change its address)
+      : "=&s"(o.r0), "=&s"(o.r1), "=&s"(o.r2), "=&s"(o.r3), "=&s"(o.r4), "=&s"(o.r5),
+        "=&s"(o.r6), "=&s"(o.r7)
       : "s"(p), "i"(0), "i"(ROW * 4), "i"(2 * ROW * 4), "i"(3 * ROW * 4), "i"(4 * ROW * 4),
         "i"(5 * ROW * 4), "i"(6 * ROW * 4), "i"(7 * ROW * 4));
   return o;
@@ -1177,6 +1180,9 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     __builtin_amdgcn_s_setprio(3);
     const int lw = w - NCW;
     int* ring = metar;  // the shared ring (loader 0 fills it)
+    // (Measured and dropped, round 5: windows to the loaders in reverse
+    // order, so that loader 0, which also issues the metadata rows, takes the
+    // fewest -- configs[3] 97.2 / north star 81.7 ms per launch either way.)
     // chunk k = channels c0 .. c0 + ncc - 1 (cht: c0 | ncc << 20), packed
     // into its buffer at the per-channel offsets of the metadata rows
     // (loader 0 reads chunk k + MA's table entry one iteration ahead: a
@@ -1275,10 +1281,17 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (stamps) { tB = __builtin_amdgcn_s_memtime(); ts_poll += tB - tA; tA = tB; }
-      // samples first: in FX tiles the compiler's wait for the window
-      // records (it cannot see the DMAs) lands before any DMA of this iteration
-      int n = k + NBUF - 1 < nchunk ? issue_samples(k + NBUF - 1) : 0;
-      n += issue_meta(k + MA);
+      // metadata rows first (loader 0), then the chunk's windows: the rows'
+      // latency overlaps the window DMAs instead of trailing them (configs[3]
+      // stage 2 101.4 -> 96.3 ms per launch, north star 83.9 -> 82.2).  The
+      // compiler's wait for the window records (vmcnt(0): it cannot see the
+      // DMAs) is forced here, before any DMA of this iteration, on records
+      // loaded one and two chunks ago
+      if constexpr (FX)
+        asm volatile("" ::"v"(rec_next.x), "v"(rec_next.y), "v"(rec_next.z), "v"(rec_next.w),
+                     "v"(rec_next2.x), "v"(rec_next2.y), "v"(rec_next2.z), "v"(rec_next2.w));
+      int n = issue_meta(k + MA);
+      n += k + NBUF - 1 < nchunk ? issue_samples(k + NBUF - 1) : 0;
       if (k + NBUF - 1 < nchunk) n += rec_ahead(k + NBUF - 1);
       else rec_tail = 0;
 #pragma unroll
