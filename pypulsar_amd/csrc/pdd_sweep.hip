@@ -1985,10 +1985,12 @@ struct FxTables {
   int rspan = 0;                   // widest relative-shift range of a group
   int maxch = 0;
   double cost_b = 0, cost_f = 0;   // modelled cycles per time tile: channel sweep / factorised
+  double el_f = 0, el_b = 0;       // staged elements per time tile (the model's inputs)
 };
 static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v, int64_t buf_e,
                      int fx, bool force, FxTables& T) {
   if (C % fx != 0 || C < 2 * fx) return false;
+  T.el_f = T.el_b = 0;
   const int64_t NG = C / fx, DB = v.DB(), ROW = DB + 4, Tq = 64 * v.G;
   const int64_t n_dblk = cdiv(D, DB);
   // pattern of (trial, group): relative shifts r1..r3 (packed key) -> pool row
@@ -2172,13 +2174,14 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
     close();
     rows_pb = std::max(rows_pb, r0);
     // cost model of one tile of this trial block (CU cycles; calibrated on
-    // MI355X, BASELINE configs[3] and the north star, round 5): the compute
-    // waves take ~440 cycles per channel of a 48-trial u16 tile (~110 per
-    // group of 4 once factorised: the adds and LDS reads scale with C / g and
-    // with the tile's trials), the loaders ~1.0 per staged element (LDS-DMA
-    // issue and landing), and the tile pays the larger of the two plus ~7%
-    // synchronisation.  (Measured, DB 72 per-tile cycles: configs[3] g 4
-    // 1.06 M -- staging-bound --, g 2 1.54 M, north star g 2 1.72 M.)
+    // MI355X, round 5): the compute waves take ~440 cycles per channel of a
+    // 48-trial u16 tile (~110 per group of 4 once factorised: the adds and
+    // LDS reads scale with C / g and with the tile's trials), the loaders
+    // ~1.0 per staged element (LDS-DMA issue and landing); the tile pays
+    // 1.016 x the larger plus 0.203 x the smaller (the DMAs' LDS writes take
+    // LDS cycles from the compute waves' reads).  Fitted on the DB 96 tiles
+    // of configs[3] g 4 (1.37 M cycles per tile, staging-bound), the north
+    // star g 4 (1.89 M) and g 2 (2.22 M, both terms ~1.8 M).
     int64_t el_b = 0, el_f = 0;  // staged elements: channel sweep / factorised
     for (int64_t c = 0; c < C; ++c) {
       int lo_ = INT32_MAX, hi_ = INT32_MIN;
@@ -2191,10 +2194,15 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
     }
     for (const auto& ch : cw[(size_t)b])
       for (const auto& r : ch) el_f += (r[1] + 63) / 64 * 64;
+    T.el_f += (double)el_f;
+    T.el_b += (double)el_b;
     if (v.S == 8) {
       const double kc = 440.0 * (double)DB / 48.0;  // compute cycles per channel of the tile
-      cost_b += 1.07 * std::max(kc * (double)C, 1.0 * (double)el_b);
-      cost_f += 1.07 * std::max(kc * (double)C / fx, 1.0 * (double)el_f);
+      auto tile = [](double comp, double st) {
+        return 1.016 * std::max(comp, st) + 0.203 * std::min(comp, st);
+      };
+      cost_b += tile(kc * (double)C, (double)el_b);
+      cost_f += tile(kc * (double)C / fx, (double)el_f);
     } else {
       // float32 quarters (configs[1] f32: 1.18 M cycles per 56-trial tile,
       // compute-bound at ~1156 cycles per channel; staging ~1.28 per element)
@@ -2204,9 +2212,11 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
     }
   }
   // stage 1 per time tile: every pattern's Tq elements (2 KiB of eighths, 4 KiB
-  // of quarters), written once for all trial blocks at ~6.7 B per CU cycle
-  // (k_fx_patterns_lds: 4.1 TB/s)
-  cost_f += (double)T.n_pat * (double)(Tq * 16) / 6.7;
+  // of quarters), written once for all trial blocks, ~251 CU cycles per 2 KiB
+  // pattern row plus ~655 per channel group (its input rows and shift range
+  // staged once): fitted on k_fx_patterns_x, configs[3] g 4 (12.6 ms per
+  // 1.04 M-column launch) and the north star g 4 / g 2 (12.65 / 6.48 ms)
+  cost_f += ((double)T.n_pat * 251.0 + (double)NG * 655.0) * (double)Tq / 128.0;
   // the channel sweep's interleave pre-pass: every channel's Tq elements per
   // time tile, written and read once (factorised plans build their pattern
   // rows from the input directly)

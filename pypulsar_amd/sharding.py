@@ -353,9 +353,15 @@ class DMShardedSweep(object):
         return torch.cat(list(src), dim=1)
 
     def close(self):
+        """Releases the plan and drops the device buffers (planes a caller
+        still holds stay valid).  The sweep closure refers back to this
+        object, so without close() the buffers live until a garbage
+        collection."""
         if self.sw is not None:
             self.sw.close()
             self.sw = None
+        self.sweep_fn = None
+        self.x = self.full = self.planes = None
 
 
 def timeshard_edges(n_out, world, align=1024):
@@ -503,7 +509,14 @@ class TimeShardedSweep(object):
                     self.sweep_fn(self.x[:, a:b + self.max_bin], self.out[:, a:b], b - a)
             return self.out
         cur = torch.cuda.current_stream(self.device)
-        cs = copy_stream if copy_stream is not None else torch.cuda.Stream(device=self.device)
+        if copy_stream is None:
+            # one copy stream per object, created once: streams created per
+            # call end up sharing a hardware queue with the compute stream,
+            # and the chunk copies then serialise behind the sweeps
+            if getattr(self, "_copy_stream", None) is None:
+                self._copy_stream = torch.cuda.Stream(device=self.device)
+            copy_stream = self._copy_stream
+        cs = copy_stream
         landed = [torch.cuda.Event() for _ in range(nb)]
         cs.wait_stream(cur)  # the previous step's reads of hx / x are done
         with torch.cuda.stream(cs):
@@ -521,10 +534,14 @@ class TimeShardedSweep(object):
         return self.out
 
     def close(self):
+        """Releases the plan and drops the device buffers (see
+        DMShardedSweep.close)."""
         if self.sw is not None:
             self.sw.close()
             self.sw = None
-        self.hx = None
+        self.sweep_fn = None
+        self.hx = self.x = self.out = self.full = None
+        self.recv = {}
 
 
 def split_block(block_tc, n_batches, world, rank):

@@ -129,12 +129,13 @@ def test_config3_sweep_oracle_rows(gpu):
     ds.close()
 
 
-def test_northstar_g2_plane(gpu, monkeypatch):
+@pytest.mark.parametrize("factor,g_want", [(True, 4), (2, 2)])
+def test_northstar_plane(gpu, monkeypatch, factor, g_want):
     """The north-star grid (4096 ch, 2048 DMs 0-1000, DDplan2b.py:168
     arange grid spacing) at N = 2^18: the planner picks the factorised sweep
-    over groups of 2 channels (the per-lane staging instance of k_sweep_il),
-    its plane equals the channel-by-channel kernel bit for bit, and sampled
-    rows equal the oracle's per-trial channel sums."""
+    over groups of 4 channels (and groups of 2 when asked for), its plane
+    equals the channel-by-channel kernel bit for bit, and sampled rows equal
+    the oracle's per-trial channel sums."""
     from pypulsar_amd import sweep as _sweep
     monkeypatch.setitem(_sweep.TEST_SWITCHES, "poison", True)  # (tests/test_gpu_factor.py)
     import torch
@@ -146,9 +147,9 @@ def test_northstar_g2_plane(gpu, monkeypatch):
     dms = np.linspace(0.0, 1000.0, D)
     x = _u8(C, N, 13)
     xd = torch.from_numpy(x).cuda()
-    sw = DMSweep(dms, freqs, DT, dtype="u8")
+    sw = DMSweep(dms, freqs, DT, dtype="u8", factor=factor)
     g, n_pat = sw.factor_info(_lib.U8)
-    assert g == 2 and n_pat > 0, (g, n_pat)
+    assert g == g_want and n_pat > 0, (g, n_pat)
     plane = sw(xd)
     n_out = plane.shape[1]
     assert n_out == N - 14504
@@ -330,11 +331,13 @@ def test_config3_full_length_properties(gpu):
     sub.close()
 
 
-def test_northstar_full_length_g2(gpu, monkeypatch):
+@pytest.mark.parametrize("factor,g_want", [(True, 4), (2, 2)])
+def test_northstar_full_length(gpu, monkeypatch, factor, g_want):
     """The north star at its full size -- 4096 ch x 2^22 samples x 2048 DMs
     (0-1000, DDplan2b.py:168 grid spacing), 8-bit -- through the bench's own
     path (DMShardedSweep, one rank, 4 time batches of 2^20 spectra in file
-    order, pieces layout): the planner picks groups of 2 channels, the
+    order, pieces layout): the planner picks groups of 4 channels (groups of
+    2 when asked for: the other u16 instance at full length), the
     factorised sweep runs 4 launches (one per batch, ~1.04 M columns each)
     with its pattern image poisoned before every stage 1, and
     (a) every plane column equals the channel-by-channel kernel bit for bit
@@ -356,10 +359,10 @@ def test_northstar_full_length_g2(gpu, monkeypatch):
     g.manual_seed(23)
     x_tc = torch.randint(0, 256, (N, C), generator=g, device="cuda", dtype=torch.uint8)
     ds = DMShardedSweep(dms, freqs, DT, N, dtype=torch.uint8, n_batches=NB,
-                        work=trial_work(dms, 1), device="cuda")
+                        work=trial_work(dms, 1), device="cuda", factor=factor)
     assert ds.pieces and ds.n_out == N - 14504 == 4179800
-    g2, n_pat = ds.sw.factor_info(_lib.U8)
-    assert g2 == 2 and n_pat > 0, (g2, n_pat)
+    gg, n_pat = ds.sw.factor_info(_lib.U8)
+    assert gg == g_want and n_pat > 0, (gg, n_pat)
     ds.sw.set_timing(True)
     planes = ds(x_tc.view(NB, N // NB, C))
     _, launches = ds.sw.timing_read()

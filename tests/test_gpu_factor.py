@@ -130,6 +130,11 @@ def test_factor_chosen_for_config3_grid(gpu):
     g, n_pat = sw.factor_info()
     assert g == 4 and n_pat > 1024
     sw.close()
+    # the north star's grid (2048 DMs): groups of 4 as well (measured, round
+    # 5: stage 2 69.0 ms per launch against 81.2 with groups of 2)
+    sw = DMSweep(np.linspace(0, 1000, 2048), band(4096), DT, dtype="u8")
+    assert sw.factor_info()[0] == 4
+    sw.close()
 
 
 @pytest.mark.gpu
