@@ -577,7 +577,7 @@ def sweep_bench(args, cfg, rank, world, dev):
     valu_roof = VALU_LANE_OPS_T * valu_adds
     uniq_bytes = C * n_in_rank * s_in + rows * cols_rank * 4
     k_s = kern_ms * 1e-3 / steps if kern_ms > 0 else None
-    # keys of profiles/pmc_sweep.json (scripts/collect_profiles_r3.py): the
+    # keys of profiles/pmc_sweep.json (scripts/collect_profiles.py): the
     # default configs[3] line (factorised), its channel-kernel line, ...
     pmc_key = "%s_%s" % (args.config, dtype)
     if args.config == "config3" and not fx_g:
