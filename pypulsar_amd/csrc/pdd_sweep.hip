@@ -983,6 +983,30 @@ __device__ __forceinline__ int stage_il_dma_s2(uint32_t lds_dst, const float4* s
   return nq;
 }
 
+// The last rem (< 64) elements of a window: one DMA piece from a
+// wave-uniform source with lanes >= rem masked off, so nothing lands past
+// the window's end in LDS.  Returns the DMAs issued (1).
+__device__ __forceinline__ int stage_il_dma_tail(uint32_t lds_dst, const float4* src, int rem,
+                                                 uint32_t voff, int lane) {
+  if (lane < rem) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(src), "s"(lds_dst)
+        : "memory");
+  }
+  return 1;
+}
+
+#ifndef PDD_FX_EXACT
+#define PDD_FX_EXACT 1
+#endif
+
 // Synchronisation of k_sweep_il: one s_barrier per chunk.  Before barrier k
 // the loader waves retire chunk k's DMAs with a counted vmcnt (chunks k+1 ..
 // k+NBUF-2 stay in flight); after it they refill the buffer chunk k-1 used.
@@ -1162,14 +1186,23 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const int nw = __builtin_amdgcn_readlane(rec.w, 0) >> 20;
     const uint64_t sv = (uint64_t)(R + (int64_t)(rec.w & 0xfffff) * nR + (t0 + rec.x - lo));
     const uint32_t dv = img_lds + (uint32_t)((b * buf_e + rec.z) * 16);
-    const int qv = (rec.y + 63) >> 6;
+    // whole 64-element pieces, then the window's last rv < 64 elements as
+    // one piece under an EXEC mask: windows sit back to back in the buffer
+    // (PDD_FX_EXACT; else every window takes whole pieces)
+    const int qv = PDD_FX_EXACT ? rec.y >> 6 : (rec.y + 63) >> 6;
+    const int rv = PDD_FX_EXACT ? rec.y & 63 : 0;
     int n = 0;
     for (int i = first; i < nw; i += step) {
       const uint32_t lo32 = __builtin_amdgcn_readlane((uint32_t)sv, i);
       const uint32_t hi32 = __builtin_amdgcn_readlane((uint32_t)(sv >> 32), i);
-      n += stage_il_dma_s2(__builtin_amdgcn_readlane(dv, i),
-                           (const float4*)(((uint64_t)hi32 << 32) | lo32),
-                           __builtin_amdgcn_readlane(qv, i), voff16);
+      const float4* src = (const float4*)(((uint64_t)hi32 << 32) | lo32);
+      const uint32_t dst = __builtin_amdgcn_readlane(dv, i);
+      const int nq = __builtin_amdgcn_readlane(qv, i);
+      n += stage_il_dma_s2(dst, src, nq, voff16);
+      if constexpr (PDD_FX_EXACT) {
+        const int rem = __builtin_amdgcn_readlane(rv, i);
+        if (rem) n += stage_il_dma_tail(dst + (uint32_t)nq * 1024u, src + nq * 64, rem, voff16, lane);
+      }
     }
     return n;
   };
@@ -2083,6 +2116,9 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
   std::vector<std::vector<int>> chunks((size_t)n_dblk);
   std::vector<std::vector<std::vector<std::array<int, 4>>>> cw((size_t)n_dblk);
   auto gran = [&](int span) -> int64_t { return (Tq + span + 63) / 64 * 64; };
+  // a pattern window takes exactly its Tq + span elements of the chunk
+  // buffer: its last DMA piece lands under an EXEC mask (k_sweep_il fx_issue)
+  auto gran_fx = [&](int span) -> int64_t { return PDD_FX_EXACT ? Tq + span : gran(span); };
   int64_t rows_pb = 0;
   double cost_b = 0, cost_f = 0;
   for (int64_t b = 0; b < n_dblk; ++b) {
@@ -2123,7 +2159,7 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
     };
     auto need_of = [&](const std::vector<std::array<int, 3>>& w) {
       int64_t n = 0;
-      for (auto& x : w) n += gran(x[2]);
+      for (auto& x : w) n += gran_fx(x[2]);
       return n;
     };
     // one row (group g, or a pad group for g < 0) with its windows
@@ -2134,7 +2170,7 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
       for (size_t i = 0; i < w.size(); ++i) {
         off[i] = used;
         rec.push_back({w[i][1], (int)(Tq + w[i][2]), (int)used, w[i][0]});
-        used += gran(w[i][2]);
+        used += gran_fx(w[i][2]);
       }
       for (int64_t j = 0; j < DB; ++j) {
         int o = (int)(16 * off[0]);
