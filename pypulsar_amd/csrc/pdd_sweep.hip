@@ -30,6 +30,7 @@
 #include <cstring>
 #include <type_traits>
 #include <unordered_map>
+#include <map>
 #include <utility>
 #include <vector>
 
@@ -1003,9 +1004,6 @@ __device__ __forceinline__ int stage_il_dma_tail(uint32_t lds_dst, const float4*
   return 1;
 }
 
-#ifndef PDD_FX_EXACT
-#define PDD_FX_EXACT 1
-#endif
 
 // Synchronisation of k_sweep_il: one s_barrier per chunk.  Before barrier k
 // the loader waves retire chunk k's DMAs with a counted vmcnt (chunks k+1 ..
@@ -1187,10 +1185,11 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const uint64_t sv = (uint64_t)(R + (int64_t)(rec.w & 0xfffff) * nR + (t0 + rec.x - lo));
     const uint32_t dv = img_lds + (uint32_t)((b * buf_e + rec.z) * 16);
     // whole 64-element pieces, then the window's last rv < 64 elements as
-    // one piece under an EXEC mask: windows sit back to back in the buffer
-    // (PDD_FX_EXACT; else every window takes whole pieces)
-    const int qv = PDD_FX_EXACT ? rec.y >> 6 : (rec.y + 63) >> 6;
-    const int rv = PDD_FX_EXACT ? rec.y & 63 : 0;
+    // one piece under an EXEC mask: windows sit back to back in the buffer.
+    // (Every window in whole pieces, round 4's layout: configs[3] stage 2
+    // 99.25 against 95.36 ms per launch, north star 69.17 against 64.94.)
+    const int qv = rec.y >> 6;
+    const int rv = rec.y & 63;
     int n = 0;
     for (int i = first; i < nw; i += step) {
       const uint32_t lo32 = __builtin_amdgcn_readlane((uint32_t)sv, i);
@@ -1199,10 +1198,8 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       const uint32_t dst = __builtin_amdgcn_readlane(dv, i);
       const int nq = __builtin_amdgcn_readlane(qv, i);
       n += stage_il_dma_s2(dst, src, nq, voff16);
-      if constexpr (PDD_FX_EXACT) {
-        const int rem = __builtin_amdgcn_readlane(rv, i);
-        if (rem) n += stage_il_dma_tail(dst + (uint32_t)nq * 1024u, src + nq * 64, rem, voff16, lane);
-      }
+      const int rem = __builtin_amdgcn_readlane(rv, i);
+      if (rem) n += stage_il_dma_tail(dst + (uint32_t)nq * 1024u, src + nq * 64, rem, voff16, lane);
     }
     return n;
   };
@@ -2118,7 +2115,7 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
   auto gran = [&](int span) -> int64_t { return (Tq + span + 63) / 64 * 64; };
   // a pattern window takes exactly its Tq + span elements of the chunk
   // buffer: its last DMA piece lands under an EXEC mask (k_sweep_il fx_issue)
-  auto gran_fx = [&](int span) -> int64_t { return PDD_FX_EXACT ? Tq + span : gran(span); };
+  auto gran_fx = [&](int span) -> int64_t { return Tq + span; };
   int64_t rows_pb = 0;
   double cost_b = 0, cost_f = 0;
   for (int64_t b = 0; b < n_dblk; ++b) {
@@ -2186,26 +2183,63 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
       }
       ++nrow;
     };
-    // a pair of rows into the open chunk (closing it first if they do not fit)
-    auto place_pair = [&](int64_t ga, const std::vector<std::array<int, 3>>& wa, int64_t gb,
-                          const std::vector<std::array<int, 3>>& wb) -> bool {
-      const int64_t need = need_of(wa) + need_of(wb);
-      const int64_t nwin = (int64_t)(wa.size() + wb.size());
-      if (need > buf_e || nwin > kFxWin) return false;
-      if (nrow + 2 > v.CC || used + need > buf_e || (int64_t)rec.size() + nwin > kFxWin) close();
-      place(ga, wa);
-      place(gb, wb);
-      return true;
-    };
-    std::vector<std::array<int, 3>> wa, wb, wz;
+    // Best-fit packing: a plane row sums over all groups and the sums are
+    // exact in any order (float32 plans: regrouped within tolerance), so the
+    // groups go into the chunks in any order.  Each chunk is filled with
+    // pairs: the largest remaining group that fits, then the largest
+    // partner that fits beside it; a group with no partner closes the chunk
+    // (or, alone in a fresh chunk, takes a pad group).  (Measured, round 5:
+    // configs[3] 305 -> 256 chunks per trial block, stage 2 95.1 ms either
+    // way; north star 461 -> 361, 65.2 -> 63.1 ms; configs[1] f32 23.9 ->
+    // 23.7 ms.  Best fit among the 16 lowest unplaced groups only, to keep
+    // neighbouring trial blocks in step: configs[3] 97.0 ms.)
+    std::vector<std::array<int, 3>> wz;
     windows(-1, wz);
-    for (int64_t g = 0; g < NG; g += 2) {
-      windows(g, wa);
-      windows(g + 1, wb);  // g + 1 == NG: the pad group
-      if (place_pair(g, wa, g + 1 < NG ? g + 1 : -1, wb)) continue;
-      // the pair does not fit one buffer: each group with a pad group
-      if (!place_pair(g, wa, -1, wz)) return false;
-      if (g + 1 < NG && !place_pair(g + 1, wb, -1, wz)) return false;
+    {
+      std::vector<std::vector<std::array<int, 3>>> wg((size_t)NG);
+      std::multimap<int64_t, int64_t> pool;  // need -> group
+      for (int64_t g = 0; g < NG; ++g) {
+        windows(g, wg[(size_t)g]);
+        pool.emplace(need_of(wg[(size_t)g]), g);
+      }
+      const int64_t need_z = need_of(wz);
+      auto take = [&](int64_t room, int64_t wroom) -> int64_t {
+        auto it = pool.upper_bound(room);
+        while (it != pool.begin()) {
+          --it;
+          if ((int64_t)wg[(size_t)it->second].size() <= wroom) {
+            const int64_t g = it->second;
+            pool.erase(it);
+            return g;
+          }
+        }
+        return -1;
+      };
+      while (!pool.empty()) {
+        const bool fresh = nrow == 0;
+        const int64_t room = buf_e - used, wroom = kFxWin - (int64_t)rec.size();
+        const int64_t a = nrow + 2 <= v.CC ? take(room, wroom) : -1;
+        if (a < 0) {
+          if (fresh) return false;  // a group that does not fit an empty buffer
+          close();
+          continue;
+        }
+        const auto& w_a = wg[(size_t)a];
+        const int64_t na = need_of(w_a);
+        const int64_t bg = take(room - na, wroom - (int64_t)w_a.size());
+        if (bg >= 0) {
+          place(a, w_a);
+          place(bg, wg[(size_t)bg]);
+        } else if (fresh && na + need_z <= room && (int64_t)w_a.size() + 1 <= wroom) {
+          place(a, w_a);
+          place(-1, wz);
+        } else if (fresh) {
+          return false;
+        } else {
+          pool.emplace(na, a);
+          close();
+        }
+      }
     }
     close();
     rows_pb = std::max(rows_pb, r0);
