@@ -2183,62 +2183,120 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
       }
       ++nrow;
     };
-    // Best-fit packing: a plane row sums over all groups and the sums are
-    // exact in any order (float32 plans: regrouped within tolerance), so the
-    // groups go into the chunks in any order.  Each chunk is filled with
-    // pairs: the largest remaining group that fits, then the largest
-    // partner that fits beside it; a group with no partner closes the chunk
-    // (or, alone in a fresh chunk, takes a pad group).  (Measured, round 5:
-    // configs[3] 305 -> 256 chunks per trial block, stage 2 95.1 ms either
-    // way; north star 461 -> 361, 65.2 -> 63.1 ms; configs[1] f32 23.9 ->
-    // 23.7 ms.  Best fit among the 16 lowest unplaced groups only, to keep
+    // Packing: a plane row sums over all groups and the sums are exact in
+    // any order (float32 plans: regrouped within tolerance), so the groups
+    // go into the chunks in any order, in pairs.  Two packings are built
+    // per trial block and the one with the lower modelled time is placed:
+    //  - best fit: the largest remaining group that fits, then the largest
+    //    partner that fits beside it (fewest chunks);
+    //  - balanced: the largest remaining group, then the SMALLEST partner
+    //    that fits, so every chunk mixes large and small window sets and its
+    //    compute (groups) tracks its staging (elements).
+    // A chunk's compute overlaps the next chunk's staging, so the model sums
+    // max(compute of chunk k, staging of chunk k + 1) plus a fixed cost per
+    // chunk.  A group with no partner closes the chunk (or, alone in a fresh
+    // chunk, takes a pad group).  (Measured, round 5, stage 2 per launch:
+    // best fit / balanced / the model's choice, configs[3] 93.55 / 92.53 /
+    // 92.42 ms, north star 62.02 / 66.95 / 61.77 ms.  Best fit over in-order
+    // pairs, configs[3] 305 -> 256 chunks per trial block, stage 2 95.1 ms
+    // either way; north star 461 -> 361, 65.2 -> 63.1 ms; configs[1] f32 23.9
+    // -> 23.7 ms.  Best fit among the 16 lowest unplaced groups only, to keep
     // neighbouring trial blocks in step: configs[3] 97.0 ms.)
     std::vector<std::array<int, 3>> wz;
     windows(-1, wz);
     {
       std::vector<std::vector<std::array<int, 3>>> wg((size_t)NG);
-      std::multimap<int64_t, int64_t> pool;  // need -> group
+      std::vector<int64_t> need_g((size_t)NG);
       for (int64_t g = 0; g < NG; ++g) {
         windows(g, wg[(size_t)g]);
-        pool.emplace(need_of(wg[(size_t)g]), g);
+        need_g[(size_t)g] = need_of(wg[(size_t)g]);
       }
       const int64_t need_z = need_of(wz);
-      auto take = [&](int64_t room, int64_t wroom) -> int64_t {
-        auto it = pool.upper_bound(room);
-        while (it != pool.begin()) {
-          --it;
-          if ((int64_t)wg[(size_t)it->second].size() <= wroom) {
-            const int64_t g = it->second;
-            pool.erase(it);
-            return g;
+      auto nw = [&](int64_t g) -> int64_t { return g < 0 ? 1 : (int64_t)wg[(size_t)g].size(); };
+      auto nd = [&](int64_t g) -> int64_t { return g < 0 ? need_z : need_g[(size_t)g]; };
+      // chunks as group lists (-1: a pad group); false when a group cannot fit
+      auto pack = [&](bool balanced, std::vector<std::vector<int64_t>>& out) -> bool {
+        out.clear();
+        std::multimap<int64_t, int64_t> pool;  // need -> group
+        for (int64_t g = 0; g < NG; ++g) pool.emplace(need_g[(size_t)g], g);
+        auto largest = [&](int64_t room, int64_t wroom) -> int64_t {
+          auto it = pool.upper_bound(room);
+          while (it != pool.begin()) {
+            --it;
+            if (nw(it->second) <= wroom) {
+              const int64_t g = it->second;
+              pool.erase(it);
+              return g;
+            }
+          }
+          return -1;
+        };
+        auto smallest = [&](int64_t room, int64_t wroom) -> int64_t {
+          for (auto it = pool.begin(); it != pool.end() && it->first <= room; ++it)
+            if (nw(it->second) <= wroom) {
+              const int64_t g = it->second;
+              pool.erase(it);
+              return g;
+            }
+          return -1;
+        };
+        std::vector<int64_t> cur;
+        int64_t used_c = 0, win_c = 0;
+        auto flush = [&]() {
+          out.push_back(cur);
+          cur.clear();
+          used_c = win_c = 0;
+        };
+        while (!pool.empty()) {
+          const bool fresh = cur.empty();
+          const int64_t room = buf_e - used_c, wroom = kFxWin - win_c;
+          const int64_t a = (int64_t)cur.size() + 2 <= v.CC ? largest(room, wroom) : -1;
+          if (a < 0) {
+            if (fresh) return false;
+            flush();
+            continue;
+          }
+          const int64_t bg = balanced ? smallest(room - nd(a), wroom - nw(a))
+                                      : largest(room - nd(a), wroom - nw(a));
+          if (bg >= 0 || (fresh && nd(a) + need_z <= room && nw(a) + 1 <= wroom)) {
+            cur.push_back(a);
+            cur.push_back(bg);
+            used_c += nd(a) + nd(bg);
+            win_c += nw(a) + nw(bg);
+          } else if (fresh) {
+            return false;
+          } else {
+            pool.emplace(nd(a), a);
+            flush();
           }
         }
-        return -1;
+        if (!cur.empty()) flush();
+        return true;
       };
-      while (!pool.empty()) {
-        const bool fresh = nrow == 0;
-        const int64_t room = buf_e - used, wroom = kFxWin - (int64_t)rec.size();
-        const int64_t a = nrow + 2 <= v.CC ? take(room, wroom) : -1;
-        if (a < 0) {
-          if (fresh) return false;  // a group that does not fit an empty buffer
-          close();
-          continue;
-        }
-        const auto& w_a = wg[(size_t)a];
-        const int64_t na = need_of(w_a);
-        const int64_t bg = take(room - na, wroom - (int64_t)w_a.size());
-        if (bg >= 0) {
-          place(a, w_a);
-          place(bg, wg[(size_t)bg]);
-        } else if (fresh && na + need_z <= room && (int64_t)w_a.size() + 1 <= wroom) {
-          place(a, w_a);
-          place(-1, wz);
-        } else if (fresh) {
-          return false;
-        } else {
-          pool.emplace(na, a);
-          close();
-        }
+      const double kc_g = v.S == 8 ? 440.0 * (double)DB / 48.0 : 1156.0 * (double)DB / 56.0;
+      const double st_e = v.S == 8 ? 1.0 : 1.28;
+      auto model = [&](const std::vector<std::vector<int64_t>>& ch) -> double {
+        auto bytes = [&](const std::vector<int64_t>& c) {
+          int64_t n = 0;
+          for (int64_t g : c) n += nd(g);
+          return (double)n;
+        };
+        double t = ch.empty() ? 0.0 : st_e * bytes(ch[0]);
+        for (size_t k = 0; k < ch.size(); ++k)
+          t += std::max(kc_g * (double)ch[k].size(), k + 1 < ch.size() ? st_e * bytes(ch[k + 1]) : 0.0) +
+               1200.0;
+        return t;
+      };
+      // (float32 tiles keep best fit: balanced chunks measured 23.24 -> 24.08
+      // ms per configs[1] launch although the model preferred them)
+      std::vector<std::vector<int64_t>> ch_f, ch_b;
+      const bool ok_f = pack(false, ch_f);
+      const bool ok_b = v.S == 8 && pack(true, ch_b);
+      if (!ok_f && !ok_b) return false;
+      const auto& ch = !ok_b ? ch_f : (!ok_f ? ch_b : (model(ch_b) < model(ch_f) ? ch_b : ch_f));
+      for (const auto& c : ch) {
+        for (int64_t g : c) place(g, g < 0 ? wz : wg[(size_t)g]);
+        close();
       }
     }
     close();
