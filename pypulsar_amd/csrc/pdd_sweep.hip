@@ -705,6 +705,7 @@ __global__ __launch_bounds__(256) void k_fx_patterns(const uint4* __restrict__ R
 // pattern row's elements stage 2 reads (fx_build): kFxE-element blocks
 // outside that range are not written.
 constexpr int kFxE = 512, kFxRspan = 512;
+
 // float32 stage 1 (k_fx_patterns_xf) builds 1024-element blocks: configs[1]
 // f32 7.31 -> 7.10 ms per launch against 512 (8-bit stage 1: 512 best, 12.5
 // against 14.2 ms at 1024)
@@ -832,8 +833,14 @@ __global__ __launch_bounds__(256) void k_fx_patterns_x(const InT* __restrict__ x
         const uint4 a = L[e - lo], b = L[W + e - lo + q.y];
         const uint4 c = FXG > 2 ? L[2 * W + e - lo + q.z] : make_uint4(0u, 0u, 0u, 0u);
         const uint4 d = FXG > 3 ? L[3 * W + e - lo + q.w] : make_uint4(0u, 0u, 0u, 0u);
-        P[(int64_t)p * nR + j] = make_uint4(a.x + b.x + c.x + d.x, a.y + b.y + c.y + d.y,
-                                            a.z + b.z + c.z + d.z, a.w + b.w + c.w + d.w);
+        // non-temporal: the pattern image is read back only after the whole
+        // stage (12.6 against 13.0 ms per configs[3] launch, same box; the
+        // float32 stage 1 measured 8.6 ms with it against 7.5 without, on
+        // another box, so it keeps plain stores)
+        typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+        const u32x4v sv = {a.x + b.x + c.x + d.x, a.y + b.y + c.y + d.y, a.z + b.z + c.z + d.z,
+                           a.w + b.w + c.w + d.w};
+        __builtin_nontemporal_store(sv, reinterpret_cast<u32x4v*>(P + (int64_t)p * nR + j));
       }
     }
   }
