@@ -1045,8 +1045,11 @@ __host__ __device__ constexpr int il_meta_bytes(int nbuf, int cc, int db) {
 // (8 x 4 groups).  Factorised sweeps (XI): band b of XCD x is global band
 // 8b + x, so the eight XCDs sweep eight ADJACENT bands with the same
 // trial-block groups at the same time and the windows two neighbouring bands
-// share are fetched from HBM once, into the Infinity Cache (4 x 2 groups;
-// DESIGN.md §3).  Leftover time tiles (n_tblk % 8) follow in natural order.
+// share are fetched from HBM once, into the Infinity Cache (8 x 2 groups
+// since the chunk packing orders each trial block's groups by its own
+// windows, so that neighbouring trial blocks no longer stage the same
+// group at the same time: configs[3] 94.23 -> 93.03 ms per launch, north
+// star 61.34 -> 59.20 ms, L2-side fetch 478 -> 412 GB).  Leftover time tiles (n_tblk % 8) follow in natural order.
 #ifndef PDD_IL_GT
 #define PDD_IL_GT 8
 #endif
@@ -1054,7 +1057,7 @@ __host__ __device__ constexpr int il_meta_bytes(int nbuf, int cc, int db) {
 #define PDD_IL_GJ 4
 #endif
 #ifndef PDD_FX_GT
-#define PDD_FX_GT 4
+#define PDD_FX_GT 8
 #endif
 #ifndef PDD_FX_GJ
 #define PDD_FX_GJ 2
