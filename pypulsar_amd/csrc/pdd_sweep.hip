@@ -2128,6 +2128,7 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
   auto gran_fx = [&](int span) -> int64_t { return Tq + span; };
   int64_t rows_pb = 0;
   double cost_b = 0, cost_f = 0;
+  std::vector<int64_t> prev_seq;  // the even trial block's group order
   for (int64_t b = 0; b < n_dblk; ++b) {
     std::vector<int>& M = rows_of[(size_t)b];
     int64_t r0 = 0, nrow = 0, used = 0;
@@ -2299,12 +2300,44 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
       };
       // (float32 tiles keep best fit: balanced chunks measured 23.24 -> 24.08
       // ms per configs[1] launch although the model preferred them)
-      std::vector<std::vector<int64_t>> ch_f, ch_b;
+      std::vector<std::vector<int64_t>> ch_f, ch_b, ch_r;
       const bool ok_f = pack(false, ch_f);
       const bool ok_b = v.S == 8 && pack(true, ch_b);
       if (!ok_f && !ok_b) return false;
-      const auto& ch = !ok_b ? ch_f : (!ok_f ? ch_b : (model(ch_b) < model(ch_f) ? ch_b : ch_f));
-      for (const auto& c : ch) {
+      const auto* ch = !ok_b ? &ch_f : (!ok_f ? &ch_b : (model(ch_b) < model(ch_f) ? &ch_b : &ch_f));
+      // The second trial block of an XCD tile group (PDD_FX_GJ = 2) stages
+      // its groups in the first block's order, re-chunked to its own window
+      // sizes, so the two blocks' concurrent tiles stage the same group's
+      // pattern rows at about the same time (L2 hits) -- unless that costs
+      // it more than 5% more chunks than its own packing.  (Measured, round
+      // 5: configs[3] stage 2 90.84 -> 88.69 ms per launch, L2-side fetch 418
+      // -> 329 GB, +2% chunks; the north star, +11% chunks, 59.01 -> 59.99 ms
+      // with it, so it keeps its own packing.)
+      if (PDD_FX_GJ == 2 && (b & 1) && !prev_seq.empty()) {
+        bool ok = true;
+        std::vector<int64_t> cur;
+        int64_t used_c = 0, win_c = 0;
+        for (size_t i = 0; i + 1 < prev_seq.size() && ok; i += 2) {
+          const int64_t ga = prev_seq[i], gb = prev_seq[i + 1];
+          const int64_t need = nd(ga) + nd(gb), w = nw(ga) + nw(gb);
+          if (need > buf_e || w > kFxWin) { ok = false; break; }
+          if ((int64_t)cur.size() + 2 > v.CC || used_c + need > buf_e || win_c + w > kFxWin) {
+            ch_r.push_back(cur);
+            cur.clear();
+            used_c = win_c = 0;
+          }
+          cur.push_back(ga);
+          cur.push_back(gb);
+          used_c += need;
+          win_c += w;
+        }
+        if (ok && !cur.empty()) ch_r.push_back(cur);
+        if (ok && (double)ch_r.size() <= 1.05 * (double)ch->size()) ch = &ch_r;
+      }
+      prev_seq.clear();
+      if (!(b & 1))
+        for (const auto& c : *ch) prev_seq.insert(prev_seq.end(), c.begin(), c.end());
+      for (const auto& c : *ch) {
         for (int64_t g : c) place(g, g < 0 ? wz : wg[(size_t)g]);
         close();
       }
