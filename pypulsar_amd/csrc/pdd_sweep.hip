@@ -2026,9 +2026,10 @@ struct FxTables {
   int maxch = 0;
   double cost_b = 0, cost_f = 0;   // modelled cycles per time tile: channel sweep / factorised
   double el_f = 0, el_b = 0;       // staged elements per time tile (the model's inputs)
+  double pair_ratio = 1.0;         // mean chunks of the re-chunked pair order / own packing
 };
 static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v, int64_t buf_e,
-                     int fx, bool force, FxTables& T) {
+                     int fx, bool force, FxTables& T, bool pairs = true) {
   if (C % fx != 0 || C < 2 * fx) return false;
   T.el_f = T.el_b = 0;
   const int64_t NG = C / fx, DB = v.DB(), ROW = DB + 4, Tq = 64 * v.G;
@@ -2129,6 +2130,8 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
   int64_t rows_pb = 0;
   double cost_b = 0, cost_f = 0;
   std::vector<int64_t> prev_seq;  // the even trial block's group order
+  double ratio_sum = 0;            // (pair order) replayed / own chunks, summed over odd blocks
+  int64_t ratio_n = 0;
   for (int64_t b = 0; b < n_dblk; ++b) {
     std::vector<int>& M = rows_of[(size_t)b];
     int64_t r0 = 0, nrow = 0, used = 0;
@@ -2308,12 +2311,14 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
       // The second trial block of an XCD tile group (PDD_FX_GJ = 2) stages
       // its groups in the first block's order, re-chunked to its own window
       // sizes, so the two blocks' concurrent tiles stage the same group's
-      // pattern rows at about the same time (L2 hits) -- unless that costs
-      // it more than 5% more chunks than its own packing.  (Measured, round
-      // 5: configs[3] stage 2 90.84 -> 88.69 ms per launch, L2-side fetch 418
-      // -> 329 GB, +2% chunks; the north star, +11% chunks, 59.01 -> 59.99 ms
-      // with it, so it keeps its own packing.)
-      if (PDD_FX_GJ == 2 && (b & 1) && !prev_seq.empty()) {
+      // pattern rows at about the same time (L2 hits).  The plan uses it
+      // only where the re-chunked orders cost at most 5% more chunks than
+      // the blocks' own packings on average (fx_build runs again without it
+      // otherwise).  (Measured, round 5: configs[3], +2% chunks, stage 2
+      // 90.84 -> 88.69 ms per launch, L2-side fetch 418 -> 329 GB; the north
+      // star, +11% chunks, 59.01 -> 59.99 ms with it; a 2.5% per-block gate
+      // instead: configs[3] 90.48 -> 91.08, north star 60.76 -> 59.44.)
+      if (pairs && PDD_FX_GJ == 2 && (b & 1) && !prev_seq.empty()) {
         bool ok = true;
         std::vector<int64_t> cur;
         int64_t used_c = 0, win_c = 0;
@@ -2332,7 +2337,11 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
           win_c += w;
         }
         if (ok && !cur.empty()) ch_r.push_back(cur);
-        if (ok && (double)ch_r.size() <= 1.05 * (double)ch->size()) ch = &ch_r;
+        if (ok) {
+          ratio_sum += (double)ch_r.size() / (double)std::max<size_t>(1, ch->size());
+          ++ratio_n;
+          ch = &ch_r;
+        }
       }
       prev_seq.clear();
       if (!(b & 1))
@@ -2394,6 +2403,7 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
   cost_b += (double)C * (double)(Tq * 16) * 2.0 / 6.7;
   T.cost_b = cost_b;
   T.cost_f = cost_f;
+  T.pair_ratio = ratio_n ? ratio_sum / (double)ratio_n : 1.0;
   if (!force && cost_f > 0.9 * cost_b) return false;
   T.rows_pb = rows_pb;
   T.mt.assign((size_t)(n_dblk * rows_pb * ROW), 0);
@@ -2626,9 +2636,15 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
         for (const Variant& f : fc) {
           const int64_t room_f = lds_budget(f) - il_meta_bytes(f.NBUF, f.CC, f.DB());
           const int64_t buf_f = std::max<int64_t>(0, room_f / (f.NBUF * 16) / 64 * 64);
-          if (!(flags & PDD_SWEEP_FACTOR_G2) && fx_build(host_table, D, C, f, buf_f, 4, force, T))
+          // (the pair order of the trial blocks is kept where it costs <= 5%
+          // more chunks on average, fx_build)
+          auto build = [&](int g, FxTables& X) {
+            if (!fx_build(host_table, D, C, f, buf_f, g, force, X)) return false;
+            return X.pair_ratio <= 1.05 || fx_build(host_table, D, C, f, buf_f, g, force, X, false);
+          };
+          if (!(flags & PDD_SWEEP_FACTOR_G2) && build(4, T))
             fxg = 4;
-          if (!(flags & PDD_SWEEP_FACTOR_G4) && fx_build(host_table, D, C, f, buf_f, 2, force, T2) &&
+          if (!(flags & PDD_SWEEP_FACTOR_G4) && build(2, T2) &&
               (fxg == 0 || T2.cost_f < T.cost_f)) {
             fxg = 2;
             std::swap(T, T2);
