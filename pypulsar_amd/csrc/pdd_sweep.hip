@@ -1027,9 +1027,14 @@ __device__ __forceinline__ int stage_il_dma_tail(uint32_t lds_dst, const float4*
 // chunk's samples, and the compute waves read the shifts of chunk k after
 // the same barrier.
 __host__ __device__ constexpr int il_ma(int nbuf) { return 2 * nbuf - 2; }
-// (ring slots: chunk j's rows are written after barrier j - MA, and read up
-// to chunk j's own compute, so MA + 2 slots suffice; 4 for two buffers)
-__host__ __device__ constexpr int il_mr(int nbuf) { return nbuf <= 2 ? 4 : (nbuf <= 4 ? 8 : (nbuf <= 8 ? 16 : 32)); }
+// (ring slots: chunk j's rows are written after barrier j - MA and read by
+// the end of chunk j's compute -- factorised tiles read them a chunk early
+// -- and every wave has finished its reads of chunk j before barrier j + 1,
+// after which chunk j + MA + 1 may overwrite the slot: MA + 1 slots suffice.
+// Two buffers: 3 slots; the fourth slot's 3.2 KiB went to the chunk buffers,
+// configs[3] stage 2 90.76 -> 90.08 ms, north star 59.42 -> 58.57 ms per
+// launch.)
+__host__ __device__ constexpr int il_mr(int nbuf) { return nbuf <= 2 ? 3 : (nbuf <= 4 ? 8 : (nbuf <= 8 ? 16 : 32)); }
 __host__ __device__ constexpr int il_slot(int cc, int db) { return (cc * (db + 4) + 63) / 64 * 64; }
 __host__ __device__ constexpr int il_meta_bytes(int nbuf, int cc, int db) {
   return il_mr(nbuf) * il_slot(cc, db) * 4;

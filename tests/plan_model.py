@@ -12,7 +12,7 @@ U8 = [(0, 0, 8, 2, 6, 12, 8, 2, 4), (0, 0, 8, 2, 4, 12, 8, 2, 4), (0, 0, 4, 4, 4
 
 
 def _mr(nbuf):
-    return 4 if nbuf <= 2 else (8 if nbuf <= 4 else (16 if nbuf <= 8 else 32))
+    return 3 if nbuf <= 2 else (8 if nbuf <= 4 else (16 if nbuf <= 8 else 32))
 
 
 def _slot(cc, db):
