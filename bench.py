@@ -861,7 +861,7 @@ def rehearse_timeshard(args, cfg, dev):
             hpart.copy_(block[lo:hi])
             e2e = []
             ts.host_step(hpart, n_batches=4, copy_stream=cs)  # (untimed: first-touch of the path)
-            for _ in range(3):
+            for _ in range(5):
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 ts.host_step(hpart, n_batches=4, copy_stream=cs)
