@@ -2645,7 +2645,11 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
           // more chunks on average, fx_build)
           auto build = [&](int g, FxTables& X) {
             if (!fx_build(host_table, D, C, f, buf_f, g, force, X)) return false;
-            return X.pair_ratio <= 1.05 || fx_build(host_table, D, C, f, buf_f, g, force, X, false);
+            if (X.pair_ratio <= 1.05 || fx_build(host_table, D, C, f, buf_f, g, force, X, false))
+              return true;
+            // (the cost screen may turn the plan down without the pair order:
+            // keep it then)
+            return fx_build(host_table, D, C, f, buf_f, g, force, X);
           };
           if (!(flags & PDD_SWEEP_FACTOR_G2) && build(4, T))
             fxg = 4;
