@@ -1067,6 +1067,11 @@ __host__ __device__ constexpr int il_meta_bytes(int nbuf, int cc, int db) {
 #ifndef PDD_FX_GJ
 #define PDD_FX_GJ 2
 #endif
+// float32 factorised tiles: 8 x 1 groups (their plans do not pair trial
+// blocks: configs[1] f32 stage 2 23.45-23.53 -> 22.95-23.01 ms against 8 x 2)
+#ifndef PDD_FX_GJF
+#define PDD_FX_GJF 1
+#endif
 template <int GT = PDD_IL_GT, int GJ = PDD_IL_GJ, bool XI = false>
 __device__ __forceinline__ void il_tile_of(int bid, int n_tblk, int n_dblk, int& dblk, int& tblk) {
   const int TX = n_tblk / 8;
@@ -1171,7 +1176,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   // rate of the staging fell from 77% to 48% at unchanged kernel time.)
   int dblk, tblk;
   const int grp = blockIdx.x / per_grp;
-  il_tile_of<FX ? PDD_FX_GT : PDD_IL_GT, FX ? PDD_FX_GJ : PDD_IL_GJ, FX>(
+  il_tile_of<FX ? PDD_FX_GT : PDD_IL_GT, FX ? (U16 ? PDD_FX_GJ : PDD_FX_GJF) : PDD_IL_GJ, FX>(
       blockIdx.x - grp * per_grp, n_tblk, n_dblk, dblk, tblk);
   const float4* R = R0 + (int64_t)grp * C * nR;
   const int64_t t0 = (int64_t)tblk * Tq;
@@ -2323,7 +2328,7 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
       // 90.84 -> 88.69 ms per launch, L2-side fetch 418 -> 329 GB; the north
       // star, +11% chunks, 59.01 -> 59.99 ms with it; a 2.5% per-block gate
       // instead: configs[3] 90.48 -> 91.08, north star 60.76 -> 59.44.)
-      if (pairs && PDD_FX_GJ == 2 && (b & 1) && !prev_seq.empty()) {
+      if (pairs && v.S == 8 && PDD_FX_GJ == 2 && (b & 1) && !prev_seq.empty()) {
         bool ok = true;
         std::vector<int64_t> cur;
         int64_t used_c = 0, win_c = 0;

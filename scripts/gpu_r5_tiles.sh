@@ -11,7 +11,7 @@ CFGS=${CFGS:-config3 northstar}
 first=${CFGS%% *}
 for lib in ${LIBS:-t4x2}; do
   for c in $CFGS; do
-    A="--config $c --steps 2 --warmup 1 --no-cpu-baseline --no-e2e"
+    A="--config $c --steps ${STEPS:-2} --warmup 1 --no-cpu-baseline --no-e2e"
     PDD_DEV_LIB=build/libpdd_$lib.so timeout -k 10 300 python bench.py $A > $O/b_${lib}_$c.json 2> $O/b_${lib}_$c.err || { echo "bench $lib $c failed"; tail -3 $O/b_${lib}_$c.err; exit 1; }
   done
   if [ -z "$NOFETCH" ]; then
