@@ -650,8 +650,9 @@ def sweep_bench(args, cfg, rank, world, dev):
                                             "(= this build)" % (pmc_key, pmc.get("kernel"),
                                                                 pmc.get("commit"),
                                                                 pmc.get("src_digest")))
-                         if traffic else "no PMC entry measured on this build (source digest / "
-                                         "plan mismatch): traffic not reported",
+                         if traffic else "no profiles/pmc_sweep.json[%s] entry of this build, "
+                                         "plan and run context (%s): traffic not reported"
+                                         % (pmc_key, json.dumps(ctx, sort_keys=True)),
                          "traffic_stage1": pmc1.get("hbm_bytes_per_launch") if pmc1 else None,
                          "traffic_unit": "HBM-side bytes per launch (traffic: this kernel; "
                                          "traffic_stage1: the factorised stage 1)",
