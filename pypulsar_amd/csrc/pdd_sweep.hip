@@ -26,6 +26,7 @@
 //    back to back on ONE XCD and re-read the tile's input from that XCD's L2.
 #include <algorithm>
 #include <array>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
@@ -2414,7 +2415,16 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
   T.cost_b = cost_b;
   T.cost_f = cost_f;
   T.pair_ratio = ratio_n ? ratio_sum / (double)ratio_n : 1.0;
-  if (!force && cost_f > 0.9 * cost_b) return false;
+  // (the plan takes the factorised tables below 0.95 of the channel sweep's
+  // modelled cost: configs[1] u8 g 2 models at 0.927 and measures 18.6
+  // against 21.6 ms per step; the margin was 0.9.  Developer builds print the
+  // model's numbers with PDD_SWEEP_DEBUG bit 3.)
+#ifdef PDD_SWEEP_DEV
+  if (debug_flags() & 8)
+    fprintf(stderr, "fx_build g %d DB %lld buf %lld: n_pat %lld cost_f %.3g cost_b %.3g el_f %.3g el_b %.3g pairs %d ratio %.3f\n",
+            fx, (long long)DB, (long long)buf_e, (long long)T.n_pat, cost_f, cost_b, T.el_f, T.el_b, (int)pairs, T.pair_ratio);
+#endif
+  if (!force && cost_f > 0.95 * cost_b) return false;
   T.rows_pb = rows_pb;
   T.mt.assign((size_t)(n_dblk * rows_pb * ROW), 0);
   for (int64_t b = 0; b < n_dblk; ++b)

@@ -57,9 +57,9 @@ def test_factor_small_grids_vs_oracle(gpu, pad, descending, C, g):
 @pytest.mark.gpu
 def test_factor_config1_geometry_equals_channel_sweep(gpu):
     """BASELINE configs[1] geometry (1024 ch x 1024 DM, 0-1000 pc/cc) on 8-bit
-    data at N = 2^17, factorised (forced: at dDM ~ 1 the planner's cost model
-    keeps this grid on the channel kernel, 25k patterns for 256 groups): the
-    plane equals the channel-by-channel kernel's bit for bit, and the
+    data at N = 2^17: the planner factorises over groups of 2 (7944 patterns;
+    groups of 4, 25k patterns for 256 groups, only when forced), and both
+    planes equal the channel-by-channel kernel's bit for bit, and the
     oracle's rows."""
     import torch
     from pypulsar_amd.sweep import DMSweep
@@ -68,7 +68,8 @@ def test_factor_config1_geometry_equals_channel_sweep(gpu):
     dms = np.linspace(0, 1000, D)
     x = u8_data(C, N, 41)
     xd = torch.from_numpy(x).cuda()
-    assert DMSweep(dms, freqs, DT, dtype="u8").factor_info()[0] == 0
+    auto = DMSweep(dms, freqs, DT, dtype="u8")
+    assert auto.factor_info()[0] == 2
     fx = DMSweep(dms, freqs, DT, dtype="u8", factor="force")
     g, n_pat = fx.factor_info()
     assert g == 4 and 0 < n_pat < 32 * C
@@ -77,12 +78,14 @@ def test_factor_config1_geometry_equals_channel_sweep(gpu):
     a = fx(xd)
     b = plain(xd)
     assert torch.equal(a, b)
+    assert torch.equal(auto(xd), b)
     tab = orc.sweep_table(dms, freqs, DT)
     rows = [0, 1, 511, 777, 1023]
     want = orc.sweep_plane(x.astype(np.float64), tab[rows], 0, n_out=a.shape[1])
     np.testing.assert_array_equal(a[rows].cpu().numpy().astype(np.float64), want)
     fx.close()
     plain.close()
+    auto.close()
 
 
 @pytest.mark.gpu
