@@ -203,10 +203,12 @@ def test_config3_timeshard_8_ranks(gpu, monkeypatch):
 def test_config1_full_size_f32(gpu):
     """BASELINE configs[1] at its full size -- 1024 ch x 2^20 samples x 1024
     DMs (0-1000), float32: on integer data the float32 plane equals the exact
-    8-bit (u16-image) plane bit for bit, and sampled rows equal the fused
-    single-DM kernel (Spectra.dedispersed_series) and the oracle."""
+    8-bit plane bit for bit (both factorised over groups of 2, the planner's
+    choice, and the 8-bit channel-by-channel plane), and sampled rows equal
+    the fused single-DM kernel (Spectra.dedispersed_series) and the oracle."""
     import torch
     from oracle import spectra_oracle as orc
+    from pypulsar_amd import _lib
     from pypulsar_amd.formats.spectra import Spectra
     from pypulsar_amd.sweep import DMSweep
     C, N, D = 1024, 1 << 20, 1024
@@ -219,7 +221,13 @@ def test_config1_full_size_f32(gpu):
     pf = swf(xf)
     assert pf.shape == (D, 1034083)
     sw8 = DMSweep(dms, freqs, DT, dtype="u8")
+    assert sw8.factor_info()[0] == 2 and swf.factor_info(_lib.F32)[0] == 2
     assert torch.equal(sw8(x8), pf)
+    sw8.close()
+    ch = DMSweep(dms, freqs, DT, dtype="u8", factor=False)
+    assert ch.factor_info()[0] == 0
+    assert torch.equal(ch(x8), pf)
+    ch.close()
     s = Spectra._from_device(freqs, DT, xf)
     rows = [0, 511, 1023]
     for d in rows:
@@ -227,7 +235,6 @@ def test_config1_full_size_f32(gpu):
     want = orc.sweep_rows_inside(x, swf.table[rows], pf.shape[1])
     np.testing.assert_array_equal(pf[rows].cpu().numpy().astype(np.float64), want)
     swf.close()
-    sw8.close()
 
 
 def test_config1_fractional_f32_rows(gpu):
