@@ -311,6 +311,9 @@ def main():
                          "planner's cost model picks 4, 2 or none; off = channel by channel; "
                          "2 / 4 = that group size where it pays; force2 / force4 = that size "
                          "wherever it fits)")
+    ap.add_argument("--no-skew", action="store_true",
+                    help="factorised sweeps: plane-aligned tiles instead of delay-aligned ones "
+                         "(the A/B of DESIGN.md §3.2; the plane is identical)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true",
                     help="dmshard / timeshard: skip the PCIe-inclusive (pinned host -> H2D -> "
@@ -326,6 +329,9 @@ def main():
                          "predicted compute efficiency")
     args = ap.parse_args()
     _maybe_spawn(args)
+    if args.no_skew:
+        from pypulsar_amd import sweep as _sweep_mod
+        _sweep_mod.TEST_SWITCHES["no_skew"] = True
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

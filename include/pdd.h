@@ -203,11 +203,19 @@ int pdd_sweep_plan_create(const int32_t* host_table, int64_t D, int64_t C, int d
  * windows do not fit one LDS chunk buffer) */
 #define PDD_SWEEP_FACTOR_G2 4
 #define PDD_SWEEP_FACTOR_G4 8  /* groups of 4 channels only */
+/* with PDD_SWEEP_FACTOR: plane-aligned factorised tiles (default: each trial's
+ * time tile is skewed by its delay at a mid-band reference group, so a
+ * tile's pattern windows span less drift; the plane is identical) */
+#define PDD_SWEEP_NO_SKEW 16
 int pdd_sweep_plan_create_ex(const int32_t* host_table, int64_t D, int64_t C, int dtype, int flags,
                              pdd_sweep_plan** plan);
 /* Channels per factor group of the plan (4 or 2; 0 = channel by channel) and, if
  * n_patterns is non-null, its stage-1 pattern count. */
 int pdd_sweep_plan_factor(const pdd_sweep_plan* plan, int64_t* n_patterns);
+/* Largest per-trial time-tile skew of a factorised plan's delay-aligned tiles
+ * (samples of an eighth / quarter; 0: plane-aligned tiles or a channel plan),
+ * and, if extra_tiles is non-null, the time tiles each segment adds for it. */
+int pdd_sweep_plan_skew(const pdd_sweep_plan* plan, int64_t* extra_tiles);
 /* x: [C][N] (ld) of the plan's dtype; out: [D][ld_out] float32.
  * For PDD_U8 with PDD_PAD_VALUE every padvals[c] must be an integer in
  * [0, 255] (checked on the host side by the caller).  PDD_U16 input: unsigned

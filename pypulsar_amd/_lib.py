@@ -33,6 +33,7 @@ SWEEP_FACTOR = 1       # pdd_sweep_plan_create_ex: exact factorised 8-bit sweeps
 SWEEP_FACTOR_FORCE = 2  # ... and taken whenever the windows fit (tests)
 SWEEP_FACTOR_G2 = 4     # ... over groups of 2 channels only
 SWEEP_FACTOR_G4 = 8     # ... over groups of 4 channels only
+SWEEP_NO_SKEW = 16      # ... with plane-aligned (not delay-aligned) factorised tiles
 
 # every symbol include/pdd.h declares (checked by tests/test_abi.py)
 EXPORTS = (
@@ -46,7 +47,7 @@ EXPORTS = (
     "pdd_sp_search", "pdd_psrfits_subints", "pdd_downsample_u8", "pdd_sweep_timing_read",
     "pdd_sweep_execute_ex", "pdd_zdm_int_downsample", "pdd_downsample_u8_u16",
     "pdd_sweep_execute_ds", "pdd_subband_chain", "pdd_scratch_release",
-    "pdd_sweep_plan_create_ex", "pdd_sweep_plan_factor", "pdd_source_digest",
+    "pdd_sweep_plan_create_ex", "pdd_sweep_plan_factor", "pdd_sweep_plan_skew", "pdd_source_digest",
     "pdd_sweep_plan_set_poison", "pdd_sweep_plan_set_segment_bytes",
 )
 
@@ -89,6 +90,7 @@ _SIGS = {
     "pdd_sweep_plan_create": ([_vp, _i64, _i64, _int, ctypes.POINTER(_vp)], _int),
     "pdd_sweep_plan_create_ex": ([_vp, _i64, _i64, _int, _int, ctypes.POINTER(_vp)], _int),
     "pdd_sweep_plan_factor": ([_vp, _vp], _int),
+    "pdd_sweep_plan_skew": ([_vp, _vp], _int),
     "pdd_sweep_execute": ([_vp, _vp, _i64, _i64, _int, _vp, _vp, _i64, _i64, _vp], _int),
     "pdd_sweep_execute_ex": ([_vp, _vp, _i64, _i64, _i64, _i64, _int, _vp, _vp, _i64, _i64,
                               ctypes.c_float, _vp], _int),

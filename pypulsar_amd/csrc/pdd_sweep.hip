@@ -1144,7 +1144,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const int* __restrict__ cht, int maxch, float* __restrict__ out, int64_t ld_out, int D,
     int64_t Qs, int64_t t_base, int64_t n_out, int buf_e, int n_tblk, int n_dblk, int dbg,
     int64_t row_g, int64_t row_d, int flush_n, float out_bias, const float* __restrict__ r2_pad,
-    int64_t r2_nR, int64_t r2_ov, const int4* __restrict__ wt) {
+    int64_t r2_nR, int64_t r2_ov, const int4* __restrict__ wt, const int* __restrict__ sig) {
   // Grouped sweeps: C is the channel count of ONE group; blockIdx.x / (tiles
   // per group) is the group, whose channels are R rows [grp*C, grp*C + C),
   // whose tables are mt[grp][...], and whose trial d lands in plane row
@@ -1611,12 +1611,16 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const int d = d0 + j;
     if (d >= D) continue;
     float* orow = out + ((int64_t)grp * row_g + (int64_t)d * row_d) * ld_out + t_base;
+    // delay-aligned factorised tiles (fx_skew): trial d's tile covers the
+    // elements [t0 - sig[d], t0 - sig[d] + Tq); each element of [0, Qs) is
+    // stored by exactly one tile of the trial
+    const int64_t ts = t0 - ((FX && sig) ? (int64_t)sig[d] : 0);
 #pragma unroll
     for (int k2 = 0; k2 < S; ++k2)
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        const int64_t t = t0 + g * 64 + lane;
-        if (t < Qs && t_base + t + k2 * Qs < n_out)
+        const int64_t t = ts + g * 64 + lane;
+        if (t >= 0 && t < Qs && t_base + t + k2 * Qs < n_out)
           orow[t + k2 * Qs] = value(j, g, k2) + out_bias;
       }
   }
@@ -1688,7 +1692,8 @@ static constexpr int kLdsMax = 160 * 1024;
 
 typedef void (*sweep_il_fn)(const float4*, int64_t, int, int, const int*, const int*, int, float*,
                             int64_t, int, int64_t, int64_t, int64_t, int, int, int, int, int64_t,
-                            int64_t, int, float, const float*, int64_t, int64_t, const int4*);
+                            int64_t, int, float, const float*, int64_t, int64_t, const int4*,
+                            const int*);
 static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false) {
   if (fx) {
     // factorised stage 2: u16 eighths (8/16-bit input) or float32 quarters
@@ -1776,6 +1781,10 @@ struct pdd_sweep_plan {
   int* d_pat = nullptr;    // factorised: [n_pat][4] {c0, r1, r2, r3}
   int* d_wt = nullptr;     // factorised: [n_dblk][maxch][kFxWin][4] window records
   int* d_gtab = nullptr;   // factorised: per group first pattern + relative-shift range (LDS stage 1)
+  int* d_sig = nullptr;    // factorised, delay-aligned tiles: [Dpad] per-trial skew (fx_skew)
+  int fx_lo = 0, fx_hi = 0;  // factorised: pattern-row sample range (skewed shifts; fx_build)
+  int fx_tpad = 0;         // factorised: extra time-tile elements per segment (max skew, whole tiles)
+  int fx_sig_max = 0;      // factorised: largest per-trial skew
   int dtype = PDD_F32;     // input element type
   int input_max = 0;       // largest input value (integer input; 0 = the dtype's bound)
   int poison = 0;          // pdd_sweep_plan_set_poison: 0xFF-fill the pattern image (tests)
@@ -1806,10 +1815,24 @@ using namespace pdd;
 // by the device memory free now (plus what this stream's image / pattern
 // slots already hold): a smaller GPU or a busier one gets more, shorter
 // segments instead of a scratch allocation failure.
+// Sample range [lo, hi] of an image row around the segment's columns:
+// channel plans min(0, min bin) .. max(0, max bin); factorised plans the
+// skewed shifts' range plus the extra time tiles of delay-aligned tiles.
+static void il_lohi(const pdd_sweep_plan* p, int64_t& lo, int64_t& hi) {
+  if (p->fx) {
+    lo = p->fx_lo;
+    hi = (int64_t)p->fx_hi + p->fx_tpad;
+  } else {
+    lo = std::min(0, p->min_bin);
+    hi = std::max(0, p->max_bin);
+  }
+}
+
 static int64_t il_seg_samples(const pdd_sweep_plan* p, hipStream_t st) {
   const int Tq = 64 * p->v.G;
   const int64_t C = p->C * p->n_grp;
-  const int64_t lo = std::min(0, p->min_bin), hi = std::max(0, p->max_bin);
+  int64_t lo, hi;
+  il_lohi(p, lo, hi);
   // bytes of R per segment: 16 GiB = one segment per quarter of a 4096 x
   // 2^22 block (configs[3] at 4 time batches), few launches per step
   int64_t budget = (int64_t)16 << 30;
@@ -1863,7 +1886,8 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
   PDD_REQUIRE(!u16 || flush_n >= p->v.CC, "pdd_sweep_execute: input bound %d too large for the "
               "packed 16-bit sums", vmax);
   const int64_t C = p->C * p->n_grp;  // all channels (groups are contiguous channel ranges)
-  const int64_t lo = std::min(0, p->min_bin), hi = std::max(0, p->max_bin);
+  int64_t lo, hi;
+  il_lohi(p, lo, hi);
   // output samples per segment
   int64_t seg = ex.one_seg ? std::max<int64_t>(n_out, 1) : il_seg_samples(p, as_stream(stream));
   PDD_REQUIRE(seg > 0, "pdd_sweep_execute: delay span %lld too wide for the segment budget",
@@ -1997,7 +2021,9 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
       }
       if (hipGetLastError() != hipSuccess) { rc = -3; break; }
     }
-    const int64_t n_tblk = Qs / Tq;
+    // (delay-aligned factorised tiles: fx_tpad / Tq more time tiles, whose
+    // trials cover the columns their skew moved past the last tile)
+    const int64_t n_tblk = Qs / Tq + (p->fx ? p->fx_tpad / Tq : 0);
     const int64_t blocks = n_tblk * p->n_dblk * p->n_grp;
     if (blocks >= (1ll << 31)) { rc = -1; break; }
     pdd_sweep_plan* pm = const_cast<pdd_sweep_plan*>(p);
@@ -2009,7 +2035,7 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
                        (int)(p->fx ? p->fx_rows - 1 : p->C), (int)lo, p->d_tab,
                        p->d_bmin, p->maxch, out, ld_out, (int)p->D, Qs, t_base, t_base + cnt,
                        p->stride, (int)n_tblk, (int)p->n_dblk, dbg, row_g, row_d, flush_n, out_bias,
-                       ex.r2_pad, ex.r2_nR, ex.r2_ov, (const int4*)p->d_wt);
+                       ex.r2_pad, ex.r2_nR, ex.r2_ov, (const int4*)p->d_wt, p->d_sig);
     if (hipGetLastError() != hipSuccess) rc = -3;
     if (bracket) {
       (void)hipEventRecord(p->ev[2 * p->timed + 1], st);
@@ -2038,13 +2064,98 @@ struct FxTables {
   double cost_b = 0, cost_f = 0;   // modelled cycles per time tile: channel sweep / factorised
   double el_f = 0, el_b = 0;       // staged elements per time tile (the model's inputs)
   double pair_ratio = 1.0;         // mean chunks of the re-chunked pair order / own packing
+  // delay-aligned tiles: trial d's tile covers output elements [t0 - sig[d],
+  // t0 - sig[d] + Tq) (sig per padded trial, >= 0); the pattern rows cover
+  // samples lo_f .. hi_f (+ tpad) around the segment (fx_skew below)
+  std::vector<int> sig;
+  int sig_max = 0, lo_f = 0, hi_f = 0;
 };
+
+// Delay-aligned tiles (factorised plans).  A trial block's tile reads, at
+// group g, the windows [t0 + b[d][g], t0 + b[d][g] + Tq) of its trials: the
+// window of a pattern spans the drift of b[d][g] over the block's trials (up
+// to ~680 samples at the bottom of the north star's band against Tq = 128
+// elements).  Trial d's tile may as well cover the output elements [t0 -
+// sig[d], t0 - sig[d] + Tq) for any per-trial skew sig[d]: it then reads
+// group g at b[d][g] - sig[d].  With sig[d] = b[d][gr] - min over the block
+// (gr: a reference group near the middle of the band, the one minimising the
+// summed drift of b - sig over the groups) the drift of group g becomes
+// |drift(g) - drift(gr)|: the north star stages 27% fewer window elements,
+// configs[3] 21% (tests/plan_model.py).  The plane is the same
+// sum at the same (trial, column): only which tile produces a column changes
+// (each segment gets ceil(max sig / Tq) more time tiles; the kernel stores
+// elements inside [0, Qs) only).
+static void fx_skew(const int32_t* tab, int64_t D, int64_t C, int64_t DB, int fx,
+                    std::vector<int>& sig) {
+  const int64_t NG = C / fx, n_dblk = cdiv(D, DB);
+  sig.assign((size_t)(n_dblk * DB), 0);
+  std::vector<int> lo((size_t)NG), hi((size_t)NG);
+  for (int64_t b = 0; b < n_dblk; ++b) {
+    auto base = [&](int64_t j, int64_t g) -> int {
+      return tab[std::min(b * DB + j, D - 1) * C + g * fx];
+    };
+    // candidate reference groups: 17 evenly spaced, then the neighbourhood
+    // of the best at the finest step
+    auto drift = [&](int64_t gr) -> int64_t {
+      std::fill(lo.begin(), lo.end(), INT32_MAX);
+      std::fill(hi.begin(), hi.end(), INT32_MIN);
+      for (int64_t j = 0; j < DB; ++j) {
+        const int s = base(j, gr);
+        for (int64_t g = 0; g < NG; ++g) {
+          const int x = base(j, g) - s;
+          lo[(size_t)g] = std::min(lo[(size_t)g], x);
+          hi[(size_t)g] = std::max(hi[(size_t)g], x);
+        }
+      }
+      int64_t t = 0;
+      for (int64_t g = 0; g < NG; ++g) t += (int64_t)hi[(size_t)g] - lo[(size_t)g];
+      return t;
+    };
+    int64_t best = -1, best_t = INT64_MAX;
+    const int64_t step = std::max<int64_t>(1, NG / 16);
+    for (int64_t gr = 0; gr < NG; gr += step) {
+      const int64_t t = drift(gr);
+      if (t < best_t) { best_t = t; best = gr; }
+    }
+    for (int64_t gr = std::max<int64_t>(0, best - step + 1); gr < std::min(NG, best + step); gr += std::max<int64_t>(1, step / 8)) {
+      const int64_t t = drift(gr);
+      if (t < best_t) { best_t = t; best = gr; }
+    }
+    int mn = INT32_MAX;
+    for (int64_t j = 0; j < DB; ++j) mn = std::min(mn, base(j, best));
+    for (int64_t j = 0; j < DB; ++j) sig[(size_t)(b * DB + j)] = base(j, best) - mn;
+  }
+}
+
 static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v, int64_t buf_e,
-                     int fx, bool force, FxTables& T, bool pairs = true) {
+                     int fx, bool force, FxTables& T, bool pairs = true, bool skew = true) {
   if (C % fx != 0 || C < 2 * fx) return false;
   T.el_f = T.el_b = 0;
   const int64_t NG = C / fx, DB = v.DB(), ROW = DB + 4, Tq = 64 * v.G;
   const int64_t n_dblk = cdiv(D, DB);
+  // per-trial skew (fx_skew; all zero: tiles aligned on the plane's columns)
+  if (skew) fx_skew(tab, D, C, DB, fx, T.sig);
+  else T.sig.assign((size_t)(n_dblk * DB), 0);
+  const std::vector<int>& sig = T.sig;
+  T.sig_max = 0;
+  for (int s : sig) T.sig_max = std::max(T.sig_max, s);
+  // the group base shift of (padded trial dp, group g) as the tile reads it
+  auto bsk = [&](int64_t dp, int64_t g) -> int {
+    return tab[std::min(dp, D - 1) * C + g * fx] - sig[(size_t)dp];
+  };
+  // the pattern rows' sample range relative to the segment: every channel's
+  // shift less its trial's skew (a pattern sums its channels at r_k more)
+  int32_t lo_all = 0, hi_all = 0;
+  for (int64_t d = 0; d < D; ++d)
+    for (int64_t c = 0; c < C; ++c) {
+      lo_all = std::min(lo_all, tab[d * C + c] - sig[(size_t)d]);
+      hi_all = std::max(hi_all, tab[d * C + c] - sig[(size_t)d]);
+    }
+  // (rounded down to 16 samples: the downsampling pre-pass of the stream
+  // takes its 16-byte vector form only on aligned segment starts)
+  lo_all = -((-lo_all + 15) / 16 * 16);
+  T.lo_f = lo_all;
+  T.hi_f = hi_all;
   // pattern of (trial, group): relative shifts r1..r3 (packed key) -> pool row
   std::vector<int> pid((size_t)(D * NG));
   std::unordered_map<uint64_t, int> idx;
@@ -2101,11 +2212,8 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
     // max(0, max bin)); stage 1 skips its kFxE-element blocks outside them
     // (5-10% of the image's bytes are delay overhang no trial of the pattern
     // reads)
-    int32_t lo_all = 0, hi_all = 0;
-    for (int64_t i = 0; i < D * C; ++i) {
-      lo_all = std::min(lo_all, tab[i]);
-      hi_all = std::max(hi_all, tab[i]);
-    }
+    // (skewed: b = the base shift less the trial's skew; rows cover [lo_f,
+    // Qs + tpad + hi_f), tpad = the skew rounded up to whole time tiles)
     const size_t o = (size_t)(3 * NG + 1);
     T.gtab.resize(o + 2 * (size_t)T.n_pat);
     for (int64_t p = 0; p < T.n_pat; ++p) {
@@ -2115,7 +2223,7 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
     for (int64_t d = 0; d < D; ++d)
       for (int64_t g = 0; g < NG; ++g) {
         const size_t q = o + 2 * (size_t)pid[(size_t)(d * NG + g)];
-        const int32_t b = tab[d * C + g * fx];
+        const int32_t b = bsk(d, g);
         T.gtab[q] = std::min(T.gtab[q], b - lo_all);
         T.gtab[q + 1] = std::max(T.gtab[q + 1], b - hi_all - 64);
       }
@@ -2168,7 +2276,7 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
       for (int64_t j = 0; j < DB; ++j) {
         const int64_t d = std::min(b * DB + j, D - 1);
         const int id = pid[(size_t)(d * NG + g)];
-        const int base = tab[d * C + g * fx];
+        const int base = bsk(b * DB + j, g);
         size_t i = 0;
         while (i < w.size() && w[i][0] != id) ++i;
         if (i == w.size()) w.push_back({id, base, base});
@@ -2199,7 +2307,7 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
         if (g >= 0 && g < NG) {
           const int64_t d = std::min(b * DB + j, D - 1);
           const int id = pid[(size_t)(d * NG + g)];
-          const int base = tab[d * C + g * fx];
+          const int base = bsk(b * DB + j, g);
           size_t i = 0;
           while (w[i][0] != id) ++i;
           o = (int)(16 * (off[i] + base - w[i][1]));
@@ -2644,6 +2752,7 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
       // the channel kernel), then the channel plan's tiling.
       FxTables T, T2;
       const bool force = (flags & PDD_SWEEP_FACTOR_FORCE) != 0;
+      const bool skew = (flags & PDD_SWEEP_NO_SKEW) == 0;
       int fxg = 0;
       if ((flags & PDD_SWEEP_FACTOR) && n_grp == 1 && v.S == (dtype == PDD_F32 ? 4 : 8) &&
           il_kernel_for(v, true)) {
@@ -2659,12 +2768,12 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
           // (the pair order of the trial blocks is kept where it costs <= 5%
           // more chunks on average, fx_build)
           auto build = [&](int g, FxTables& X) {
-            if (!fx_build(host_table, D, C, f, buf_f, g, force, X)) return false;
-            if (X.pair_ratio <= 1.05 || fx_build(host_table, D, C, f, buf_f, g, force, X, false))
+            if (!fx_build(host_table, D, C, f, buf_f, g, force, X, true, skew)) return false;
+            if (X.pair_ratio <= 1.05 || fx_build(host_table, D, C, f, buf_f, g, force, X, false, skew))
               return true;
             // (the cost screen may turn the plan down without the pair order:
             // keep it then)
-            return fx_build(host_table, D, C, f, buf_f, g, force, X);
+            return fx_build(host_table, D, C, f, buf_f, g, force, X, true, skew);
           };
           if (!(flags & PDD_SWEEP_FACTOR_G2) && build(4, T))
             fxg = 4;
@@ -2689,6 +2798,10 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
         p->n_pat = T.n_pat;
         p->fx_rows = T.rows_pb;
         p->fx_rspan = T.rspan;  // stage 1 sizes its LDS to it: more workgroups per CU
+        p->fx_lo = T.lo_f;
+        p->fx_hi = T.hi_f;
+        p->fx_tpad = (int)(cdiv(T.sig_max, 64 * p->v.G) * 64 * p->v.G);
+        p->fx_sig_max = T.sig_max;
         p->maxch = T.maxch;
         tab.swap(T.mt);
         bmin.swap(T.cht);
@@ -2698,6 +2811,9 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
           e = hipMemcpy(p->d_pat, T.pat.data(), T.pat.size() * sizeof(int), hipMemcpyHostToDevice);
         if (e == hipSuccess)
           e = hipMemcpy(p->d_wt, T.wt.data(), T.wt.size() * sizeof(int), hipMemcpyHostToDevice);
+        if (e == hipSuccess && T.sig_max > 0) e = hipMalloc(&p->d_sig, T.sig.size() * sizeof(int));
+        if (e == hipSuccess && T.sig_max > 0)
+          e = hipMemcpy(p->d_sig, T.sig.data(), T.sig.size() * sizeof(int), hipMemcpyHostToDevice);
         if (e == hipSuccess && !T.gtab.empty()) e = hipMalloc(&p->d_gtab, T.gtab.size() * sizeof(int));
         if (e == hipSuccess && !T.gtab.empty())
           e = hipMemcpy(p->d_gtab, T.gtab.data(), T.gtab.size() * sizeof(int), hipMemcpyHostToDevice);
@@ -2751,6 +2867,12 @@ int pdd_sweep_plan_factor(const pdd_sweep_plan* p, int64_t* n_patterns) {
   PDD_REQUIRE(p, "pdd_sweep_plan_factor: null pointer");
   if (n_patterns) *n_patterns = p->n_pat;
   return p->fx;
+}
+
+int pdd_sweep_plan_skew(const pdd_sweep_plan* p, int64_t* extra_tiles) {
+  PDD_REQUIRE(p, "pdd_sweep_plan_skew: null pointer");
+  if (extra_tiles) *extra_tiles = p->fx ? p->fx_tpad / (64 * p->v.G) : 0;
+  return p->fx ? p->fx_sig_max : 0;
 }
 
 int pdd_sweep_plan_info(const pdd_sweep_plan* p, int64_t* info) {
@@ -2987,6 +3109,7 @@ int pdd_sweep_plan_destroy(pdd_sweep_plan* p) {
   if (p->d_pat) (void)hipFree(p->d_pat);
   if (p->d_wt) (void)hipFree(p->d_wt);
   if (p->d_gtab) (void)hipFree(p->d_gtab);
+  if (p->d_sig) (void)hipFree(p->d_sig);
   delete p;
   return 0;
 }

@@ -53,8 +53,10 @@ def _is_int_pad16(padval):
 # tests set them, e.g. with pytest's monkeypatch.setitem; production code
 # never does): poison -- factorised plans fill their pattern image with 0xFF
 # bytes before stage 1 (pdd_sweep_plan_set_poison); segment_bytes > 0 -- the
-# scratch budget of one time segment (pdd_sweep_plan_set_segment_bytes).
-TEST_SWITCHES = {"poison": False, "segment_bytes": 0}
+# scratch budget of one time segment (pdd_sweep_plan_set_segment_bytes);
+# no_skew -- factorised plans are created with plane-aligned tiles
+# (PDD_SWEEP_NO_SKEW; bench.py --no-skew, the A/B of DESIGN.md §3.2).
+TEST_SWITCHES = {"poison": False, "segment_bytes": 0, "no_skew": False}
 
 
 def _apply_test_switches(p):
@@ -74,7 +76,8 @@ class DMSweep(object):
     [C, N] device tensor of that dtype (int16 / uint16 storage for 'u16') or
     a ``Spectra``."""
 
-    def __init__(self, dms, freqs, dt, cur_dm=0.0, dtype="f32", input_max=None, factor=True):
+    def __init__(self, dms, freqs, dt, cur_dm=0.0, dtype="f32", input_max=None, factor=True,
+                 skew=True):
         """``input_max`` (integer dtypes): the largest sample value the input
         and its integer pads hold (default 255 for 'u8', 1023 for 'u16'); a
         tighter bound lets the exact packed-u16 accumulation convert less
@@ -83,7 +86,11 @@ class DMSweep(object):
         (pdd_sweep_plan_create_ex PDD_SWEEP_FACTOR; bit-identical planes);
         False forces the channel-by-channel kernel; 2 or 4: that group size
         only (still where it pays); "force2" / "force4" (= "force"): that
-        group size wherever the windows fit, paying or not (tests)."""
+        group size wherever the windows fit, paying or not (tests).
+        ``skew``: factorised plans use delay-aligned time tiles (each trial's
+        tile skewed by its delay at a mid-band group: fewer staged window
+        elements, the same plane); False keeps plane-aligned tiles
+        (PDD_SWEEP_NO_SKEW; A/B measurements and parity tests)."""
         _lib.require_gpu()
         self.dms = np.atleast_1d(np.asarray(dms, dtype=np.float64))
         self.freqs = np.asarray(freqs, dtype=np.float64)
@@ -100,6 +107,7 @@ class DMSweep(object):
             factor = "force4"
         assert factor in (True, False, 2, 4, "force2", "force4"), "bad factor %r" % (factor,)
         self.factor = factor
+        self.skew = bool(skew)
         if self.input_max is not None:
             assert dtype in ("u8", "u16") and 1 <= self.input_max <= (255 if dtype == "u8" else 1023)
         self._plans = {}
@@ -142,6 +150,8 @@ class DMSweep(object):
         if f is False:
             return 0
         flags = _lib.SWEEP_FACTOR
+        if not getattr(self, "skew", True) or TEST_SWITCHES["no_skew"]:
+            flags |= _lib.SWEEP_NO_SKEW
         if isinstance(f, str):
             flags |= _lib.SWEEP_FACTOR_FORCE
             f = int(f[-1])
@@ -157,6 +167,15 @@ class DMSweep(object):
         if g < 0:
             _lib.check(g, "pdd_sweep_plan_factor")
         return int(g), int(n.value)
+
+    def skew_info(self, code=_lib.U8):
+        """(largest per-trial tile skew, extra time tiles per segment) of the
+        plan for ``code``: (0, 0) for plane-aligned tiles (pdd_sweep_plan_skew)."""
+        n = ctypes.c_int64(0)
+        s = _lib.lib().pdd_sweep_plan_skew(self._plan(code), ctypes.byref(n))
+        if s < 0:
+            _lib.check(s, "pdd_sweep_plan_skew")
+        return int(s), int(n.value)
 
     def n_out(self, N, trim=True):
         if trim and self.max_bin > 0:

@@ -24,7 +24,8 @@ def test_flag_values_match_header():
     for name, val in (("PDD_SWEEP_FACTOR", _lib.SWEEP_FACTOR),
                       ("PDD_SWEEP_FACTOR_FORCE", _lib.SWEEP_FACTOR_FORCE),
                       ("PDD_SWEEP_FACTOR_G2", _lib.SWEEP_FACTOR_G2),
-                      ("PDD_SWEEP_FACTOR_G4", _lib.SWEEP_FACTOR_G4)):
+                      ("PDD_SWEEP_FACTOR_G4", _lib.SWEEP_FACTOR_G4),
+                      ("PDD_SWEEP_NO_SKEW", _lib.SWEEP_NO_SKEW)):
         m = re.search(r"#define %s (\d+)" % name, src)
         assert m and int(m.group(1)) == val, name
 

@@ -225,3 +225,40 @@ def test_factor_f32_config1_geometry(gpu):
     assert rel_err(a[rows].cpu().numpy(), want) <= 1e-5
     fx.close()
     plain.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pad", [0, 7, "rotate"])
+@pytest.mark.parametrize("descending", [True, False])
+@pytest.mark.parametrize("mode", ["force4", "force2"])
+def test_factor_delay_aligned_tiles(gpu, pad, descending, mode):
+    """Delay-aligned factorised tiles (pdd_sweep.hip fx_skew): each trial's
+    time tile is skewed by its delay at a mid-band reference group, here by up
+    to ~180 samples (two extra time tiles per segment), so tiles of one trial
+    block store different column ranges and the first / last tiles store only
+    part of their elements.  The plane equals the plane-aligned tiles' plane
+    and the oracle's bit for bit: value / rotate pads, trim on and off, both
+    band orders, a grid over two trial blocks with a partial second block."""
+    import torch
+    from pypulsar_amd.sweep import DMSweep
+    C, N, D = 64, 6000, 200
+    freqs = band(C, descending=descending)
+    x = u8_data(C, N, 61)
+    xd = torch.from_numpy(x).cuda()
+    dms = np.linspace(0, 60.0, D)
+    sk = DMSweep(dms, freqs, DT, dtype="u8", factor=mode)
+    al = DMSweep(dms, freqs, DT, dtype="u8", factor=mode, skew=False)
+    assert sk.factor_info()[0] == al.factor_info()[0] == int(mode[-1])
+    s_max, extra = sk.skew_info()
+    assert s_max > 128 and extra >= 2, (s_max, extra)
+    assert al.skew_info() == (0, 0)
+    tab = orc.sweep_table(dms, freqs, DT)
+    for trim in (True, False):
+        a = sk(xd, padval=pad, trim=trim)
+        b = al(xd, padval=pad, trim=trim)
+        assert torch.equal(a, b), (pad, trim)
+        want = orc.sweep_plane(x.astype(np.float64), tab, pad, n_out=a.shape[1])
+        np.testing.assert_array_equal(a.cpu().numpy().astype(np.float64), want,
+                                      err_msg="pad %r trim %s" % (pad, trim))
+    sk.close()
+    al.close()
