@@ -139,6 +139,59 @@ def cpu_baseline(C, n, dms, ntrials, dt, full_N):
     return res
 
 
+def _pinned_h2d_GBs(h, dev, reps=5):
+    """Pinned host -> device rate of ``h`` copied alone (best of ``reps``)."""
+    d = torch.empty(h.shape, dtype=h.dtype, device=dev)
+    best = None
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        d.copy_(h, non_blocking=True)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        best = el if best is None else min(best, el)
+    del d
+    return h.numel() * h.element_size() / best / 1e9
+
+
+def stream_cpu_baseline(C, ds, dms, dt, nb_gpu, D, mode, n_raw=1 << 15, ntrials=6):
+    """The stream's per-block work on the host: the oracle's
+    zero-DM (the reference's uint8 result, bin/zero_dm_filter.py:30-39, per
+    spectrum) + downsample (formats/spectra.py:329-351) of an ``n_raw``-
+    spectrum 8-bit slice, then ``ntrials`` DM trials of dedisperse(trim) +
+    channel sum (spectra.py:229-260, waterfaller.py:140), one core, C-order.
+    ``value`` extrapolates the timed sample to the GPU's per-block work: one
+    prologue + D trials per block of units D x columns x C."""
+    from oracle import spectra_oracle as orc
+    freqs = band(C)
+    rng = np.random.default_rng(1)
+    x = np.clip(np.round(rng.normal(128, 16, (n_raw, C))), 0, 255).astype(np.uint8)
+    zmode = {"wrap": "wrap", "int": "int"}.get(mode, "none")
+    t0 = time.perf_counter()
+    if mode == "float":
+        z = orc.zdm_downsample(x, ds, zero_dm=True)
+    else:
+        z = orc.zdm_int_downsample(x, ds, mode=zmode).astype(np.float64)
+    t_pro = time.perf_counter() - t0
+    pick = dms[np.linspace(0, len(dms) - 1, ntrials).astype(int)]
+    cols, t0 = [], time.perf_counter()
+    for dm in pick:
+        d, _ = orc.dedisperse(z, freqs, dt * ds, dm, padval=0, trim=True)
+        cols.append(orc.channel_sum(d).shape[0])
+        del d
+    t_tr = (time.perf_counter() - t0) / ntrials
+    n_cols = float(np.mean(cols))
+    value = D * n_cols * C / (t_pro + D * t_tr)
+    return dict(value=value, unit="samples*channels*DM/s (downsampled samples)", cores=1,
+                kind="port", cpu_model=_cpu_model(), nproc=os.cpu_count(),
+                prologue_s=t_pro, s_per_trial=t_tr,
+                sample="zero-DM (%s) + downsample %d of %d x %d u8 spectra (%.2f s), then %d DM "
+                       "trials of the grid (dedisperse(trim)+channel sum) on the %d x %d "
+                       "result (%.2f s each), float64 NumPy, 1 thread; value = one prologue "
+                       "+ %d trials per block" % (mode, ds, n_raw, C, t_pro, ntrials, C,
+                                                  z.shape[1], t_tr, D))
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -1117,10 +1170,15 @@ def search_bench(args, cfg, rank, world, dev):
 def stream_bench(args, cfg, rank, world, dev):
     """BASELINE configs[4]: continuous 8-bit blocks [block, C] from PINNED host
     memory -> async H2D (copy stream) -> fused zero-DM + downsample 2 ->
-    2048-DM sweep (pypulsar_amd.stream; default zero-DM mode 'int': the
-    reference's rounded channel mean subtracted exactly, swept on the exact
+    2048-DM sweep (pypulsar_amd.stream; default zero-DM mode 'wrap': the
+    reference's uint8 result, (x - round(mean)) mod 256, swept exactly on the
     16-bit path; --zdm float for the float32 path).  One step = one block through the
-    whole pipeline, H2D included.  Each rank streams its own data (weak)."""
+    whole pipeline, H2D included.  Each rank streams its own data (weak).
+    roofline: the block's pinned H2D against this box's pinned H2D rate (the
+    binding resource); roofline.sweep_kernel: the sweep kernel's own LDS
+    fraction in the adds it performs; cpu_baseline: the oracle's prologue +
+    trials on a bounded slice (stream_cpu_baseline)."""
+    from pypulsar_amd import _lib
     from pypulsar_amd.stream import StreamingSweep
     C, D, ds = cfg["C"], cfg["D"], cfg["ds"]
     block = args.block or cfg["N"]
@@ -1161,6 +1219,10 @@ def stream_bench(args, cfg, rank, world, dev):
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
+            # the sweep kernel's own launches, timed by the plan's HIP event
+            # pairs on the stream it runs on (its LDS fraction below)
+            st.sweep.set_timing(True, code=_lib.U16 if st.exact else _lib.F32)
+            st.sweep.timing_read()
             t0 = time.perf_counter()
         if done == args.warmup + args.steps:
             break
@@ -1168,6 +1230,8 @@ def stream_bench(args, cfg, rank, world, dev):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    k_ms, k_n = st.sweep.timing_read()
+    st.sweep.set_timing(False, code=_lib.U16 if st.exact else _lib.F32)
     if world > 1:
         el = max_over_ranks(el, dev)
     units = D * nb * C * args.steps * world
@@ -1177,6 +1241,17 @@ def stream_bench(args, cfg, rank, world, dev):
     in_rate = block * args.steps * world / el  # input spectra per second
     fx_g, fx_pat = st.sweep.factor_info(2 if st.exact else 0) if st.exact else (0, 0)
     h2d_bytes = block * C  # one 8-bit block per step over PCIe (pinned, async)
+    # the binding resource: the block's pinned H2D, against this box's own
+    # pinned H2D rate (the same bytes copied alone, best of 5)
+    h2d_peak = _pinned_h2d_GBs(chunks[0], dev)
+    h2d_at = h2d_bytes / (ms * 1e-3) / 1e9
+    # the sweep kernel alone: factorised adds per launch over its HIP-event time
+    k_adds = D * nb * C / max(1, fx_g)
+    k_launch_ms = k_ms / k_n if k_n else None
+    k_tadds = k_adds / (k_launch_ms * 1e-3) / 1e12 if k_launch_ms else None
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = stream_cpu_baseline(C, ds, dms, dt, nb, D, st.mode)
     line = {
         "metric": "DM-trial samples*channels/sec (node) + % HBM roofline",
         "value": value, "unit": "samples*channels*DM/s (downsampled samples)",
@@ -1204,18 +1279,28 @@ def stream_bench(args, cfg, rank, world, dev):
                    "downsamp": ds, "dm_trials": D, "parallelism": "tb%d" % world},
         "realtime_factor": (block * dt) / (ms * 1e-3),
         "input_spectra_per_s": in_rate,
-        "roofline": {"bound": "lds", "achieved": D * nb * C / (ms * 1e-3) / 1e12,
-                     "peak": lds_roof, "unit": "T adds/s",
-                     "frac": D * nb * C / (ms * 1e-3) / 1e12 / lds_roof, "traffic": None,
-                     "note": "whole-step time (H2D, prologue, sweep) per block; one add per "
-                             "unit against the sweep's LDS read roof (%s image)%s"
-                             % ("u16 eighths" if st.exact else "float32 quarters",
-                                "; factorised: the sweep adds 1/%d of these and the step is "
-                                "bound by the block's H2D (h2d_GBs_at_step)" % fx_g if fx_g
-                                else "")},
+        "roofline": {"bound": "pcie", "achieved": h2d_at, "peak": h2d_peak, "unit": "GB/s",
+                     "frac": h2d_at / h2d_peak if h2d_peak else None, "traffic": None,
+                     "kernel": "pinned H2D of the 8-bit block (hipMemcpyAsync on the copy "
+                               "stream)",
+                     "note": "the step's binding resource: one %d-byte block per step over "
+                             "PCIe; peak = this box's pinned H2D rate for the same bytes "
+                             "copied alone (best of 5); the prologue and the sweep run under "
+                             "the copy (sweep_kernel)" % h2d_bytes,
+                     "sweep_kernel": {
+                         "kernel": "pdd::k_sweep_il (%s)" % ("factorised stage 2, groups of %d"
+                                                             % fx_g if fx_g else
+                                                             ("u16 eighths" if st.exact else
+                                                              "float32 quarters")),
+                         "bound": "lds", "unit": "T adds/s", "peak": lds_roof,
+                         "ms_per_launch": k_launch_ms, "launches_per_step": k_n / args.steps,
+                         "adds_per_launch": k_adds, "achieved": k_tadds,
+                         "frac": k_tadds / lds_roof if k_tadds else None,
+                         "note": "adds the kernel performs (D x columns x C / g) over its own "
+                                 "HIP-event time; 8-bit factorised adds read 2 B of LDS each"}},
         "h2d_bytes_per_step": h2d_bytes,
-        "h2d_GBs_at_step": h2d_bytes / (ms * 1e-3) / 1e9,
-        "cpu_baseline": None,
+        "h2d_GBs_at_step": h2d_at,
+        "cpu_baseline": cpu,
     }
     st.close()
     _finish(args, world, line)

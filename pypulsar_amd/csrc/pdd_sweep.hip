@@ -1668,7 +1668,10 @@ static const Variant kF32Variants[] = {
 // configs[3] g 4 101.8 -> 97.2 ms per launch, north star g 2 83.3 -> 81.6
 // against DB 72; the channel kernel is 2% slower at DB 96 (configs[1] u8
 // 21.0 -> 21.5 ms), so channel plans keep DB 72.
-static const Variant kU8FxVariants[] = {{0, false, 8, 2, 8, 12, 8, 2, 4}};
+#ifndef PDD_FX_DPW
+#define PDD_FX_DPW 8
+#endif
+static const Variant kU8FxVariants[] = {{0, false, 8, 2, PDD_FX_DPW, 12, 8, 2, 4}};
 static const Variant kU8Variants[] = {
     {0, false, 8, 2, 6, 12, 8, 2, 4},   // u16 eighths, DB 72: 6 trials per compute wave in the
                                         //   registers 4 took with float totals (k_sweep_il's
@@ -2577,6 +2580,11 @@ int pdd_sweep_plan_create_grouped(const int32_t* host_table, int64_t n_grp, int6
 
 }  // extern "C"
 
+// Largest mean chunk ratio (re-chunked pair order / own packing) at which a
+// factorised plan keeps the pair order of its trial blocks (fx_build).
+#ifndef PDD_FX_PAIR_MAX
+#define PDD_FX_PAIR_MAX 1.06
+#endif
 static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int64_t C, int dtype,
                        int flags, pdd_sweep_plan** plan_out) {
   PDD_REQUIRE(host_table && plan_out, "pdd_sweep_plan_create: null pointer");
@@ -2769,7 +2777,7 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
           // more chunks on average, fx_build)
           auto build = [&](int g, FxTables& X) {
             if (!fx_build(host_table, D, C, f, buf_f, g, force, X, true, skew)) return false;
-            if (X.pair_ratio <= 1.05 || fx_build(host_table, D, C, f, buf_f, g, force, X, false, skew))
+            if (X.pair_ratio <= PDD_FX_PAIR_MAX || fx_build(host_table, D, C, f, buf_f, g, force, X, false, skew))
               return true;
             // (the cost screen may turn the plan down without the pair order:
             // keep it then)

@@ -132,9 +132,16 @@ class filterbank(object):
         """Read samples [startsamp, startsamp + len(out)) into ``out``, a
         C-contiguous host array (numpy, or a pinned torch tensor's .numpy())
         of shape [n, nchans] and the file's dtype; returns the number of whole
-        spectra read (fewer at the end of the file)."""
+        spectra read (fewer at the end of the file).  A non-contiguous
+        ``out`` is refused (ValueError): the bytes would land in a temporary
+        copy, not in ``out``."""
+        if not isinstance(out, np.ndarray) or not out.flags["C_CONTIGUOUS"]:
+            raise ValueError("read_block_into: out must be a C-contiguous numpy array")
+        if out.ndim != 2 or out.shape[1] != self.header["nchans"] or out.dtype != self.dtype:
+            raise ValueError("read_block_into: out must be [n, %d] of %s, not %s of %s"
+                             % (self.header["nchans"], self.dtype, out.shape, out.dtype))
         self.seek_to_sample(startsamp)
-        buf = memoryview(np.ascontiguousarray(out).view(np.uint8).reshape(-1))
+        buf = memoryview(out.view(np.uint8).reshape(-1))
         got = self.filfile.readinto(buf)
         return got // self.bytes_per_spectrum
 

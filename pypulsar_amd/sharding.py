@@ -466,6 +466,11 @@ class TimeShardedSweep(object):
         self.to_cm(part, self.x)
         if self.cols:
             self.sweep_fn(self.x, self.out, self.cols)
+        return self._gathered()
+
+    def _gathered(self):
+        """This rank's plane, or (``gather``) the column blocks sent to
+        ``dst`` point-to-point: ``dst`` returns the full plane."""
         if not self.gather or self.world == 1:
             return self.out
         if self.rank != self.dst:
@@ -490,12 +495,16 @@ class TimeShardedSweep(object):
         plus the max-delay overlap -- have landed: chunk k+1's copy runs
         under range k's corner turn and sweep, only chunk 0's is exposed.
         The plane equals __call__'s bit for bit (every range reads only
-        in-range samples).  Returns this rank's [D, cols] plane."""
-        assert not self.gather, "host_step returns the rank's own plane (no gather)"
+        in-range samples).  Returns this rank's [D, cols] plane (``dst`` with
+        ``gather``: the full plane, as __call__)."""
         assert tuple(hpart.shape) == (self.n_in, self.C) and hpart.dtype == self.dtype
         nb = max(1, min(int(n_batches), max(1, self.cols // self.align)))
         ce = timeshard_edges(self.cols, nb, self.align)            # column ranges (relative)
-        ie = [0] + [min(self.n_in, ce[k + 1] + self.max_bin) for k in range(nb - 1)] + [self.n_in]
+        # chunk edges rounded up to 16 spectra (capped at n_in): every chunk's
+        # corner turn starts on a 16-byte boundary and takes the 16-byte 8-bit
+        # path (pdd_corner_turn); a chunk only has to cover its range's input
+        ie = [0] + [min(self.n_in, -(-(ce[k + 1] + self.max_bin) // 16) * 16)
+                    for k in range(nb - 1)] + [self.n_in]
         if getattr(self, "hx", None) is None:
             self.hx = torch.empty((self.n_in, self.C), dtype=self.dtype, device=self.device)
         if self.device.type != "cuda":
@@ -507,7 +516,7 @@ class TimeShardedSweep(object):
                 a, b = ce[k], ce[k + 1]
                 if b > a:
                     self.sweep_fn(self.x[:, a:b + self.max_bin], self.out[:, a:b], b - a)
-            return self.out
+            return self._gathered()
         cur = torch.cuda.current_stream(self.device)
         if copy_stream is None:
             # one copy stream per object, created once: streams created per
@@ -531,7 +540,7 @@ class TimeShardedSweep(object):
             a, b = ce[k], ce[k + 1]
             if b > a:
                 self.sweep_fn(self.x[:, a:b + self.max_bin], self.out[:, a:b], b - a)
-        return self.out
+        return self._gathered()
 
     def close(self):
         """Releases the plan and drops the device buffers (see

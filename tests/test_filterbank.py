@@ -54,6 +54,16 @@ def test_round_trip(tmp_path, nbits, dtype):
     buf = np.empty((20, 32), dtype=dtype)
     assert fb.read_block_into(40, buf) == 10
     np.testing.assert_array_equal(buf[:10], x[40:])
+    # a non-contiguous or mis-shaped destination is refused, not filled
+    # through a temporary copy
+    wide = np.zeros((20, 64), dtype=dtype)
+    with pytest.raises(ValueError):
+        fb.read_block_into(0, wide[:, ::2])
+    with pytest.raises(ValueError):
+        fb.read_block_into(0, np.zeros((20, 16), dtype=dtype))
+    with pytest.raises(ValueError):
+        fb.read_block_into(0, np.zeros((20, 32), dtype=np.int64))
+    assert not wide.any()
     # re-written header bytes are identical (zero_dm_filter.py:21-27 path)
     with open(fn, "rb") as f:
         head = f.read(fb.header_size)

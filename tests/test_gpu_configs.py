@@ -338,10 +338,11 @@ def test_config3_full_length_properties(gpu):
     sub.close()
 
 
-@pytest.mark.parametrize("factor,g_want", [(True, 4), (2, 2)])
-def test_northstar_full_length(gpu, monkeypatch, factor, g_want):
+@pytest.mark.parametrize("D,factor,g_want", [(2048, True, 4), (2048, 2, 2), (4096, True, 4)])
+def test_northstar_full_length(gpu, monkeypatch, D, factor, g_want):
     """The north star at its full size -- 4096 ch x 2^22 samples x 2048 DMs
-    (0-1000, DDplan2b.py:168 grid spacing), 8-bit -- through the bench's own
+    (0-1000, DDplan2b.py:168 grid spacing), 8-bit -- and BASELINE configs[3]
+    (the same with 4096 DMs: the default bench line's exact step) through the bench's own
     path (DMShardedSweep, one rank, 4 time batches of 2^20 spectra in file
     order, pieces layout): the planner picks groups of 4 channels (groups of
     2 when asked for: the other u16 instance at full length), the
@@ -359,17 +360,20 @@ def test_northstar_full_length(gpu, monkeypatch, factor, g_want):
     from pypulsar_amd.sharding import DMShardedSweep, trial_work
     from pypulsar_amd.sweep import DMSweep
     monkeypatch.setitem(_sweep.TEST_SWITCHES, "poison", True)
-    C, N, D, NB = 4096, 1 << 22, 2048, 4
+    C, N, NB = 4096, 1 << 22, 4
     freqs = band(C)
     dms = np.linspace(0.0, 1000.0, D)
     g = torch.Generator(device="cuda")
-    g.manual_seed(23)
+    g.manual_seed(23 + D)
     x_tc = torch.randint(0, 256, (N, C), generator=g, device="cuda", dtype=torch.uint8)
     ds = DMShardedSweep(dms, freqs, DT, N, dtype=torch.uint8, n_batches=NB,
                         work=trial_work(dms, 1), device="cuda", factor=factor)
     assert ds.pieces and ds.n_out == N - 14504 == 4179800
     gg, n_pat = ds.sw.factor_info(_lib.U8)
     assert gg == g_want and n_pat > 0, (gg, n_pat)
+    # delay-aligned tiles (pdd_sweep.hip fx_skew): trials skewed by up to
+    # their block's delay drift at the reference group
+    assert ds.sw.skew_info(_lib.U8)[0] > 64
     ds.sw.set_timing(True)
     planes = ds(x_tc.view(NB, N // NB, C))
     _, launches = ds.sw.timing_read()
@@ -396,7 +400,7 @@ def test_northstar_full_length(gpu, monkeypatch, factor, g_want):
     _lib.check(_lib.lib().pdd_scratch_release(), "pdd_scratch_release")
     s = Spectra._from_device(freqs, DT, x8.float())
     del x8
-    for d in (0, 1, 1023, 1024, 2046, 2047):
+    for d in (0, 1, 1023, 1024, D - 2, D - 1):
         ser = s.dedispersed_series(dms[d], padval=0, trim=True)[:n_out]
         got = torch.cat([planes[k][d] for k in range(NB)])
         assert torch.equal(ser, got), "row %d != dedispersed_series" % d

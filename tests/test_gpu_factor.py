@@ -234,14 +234,14 @@ def test_factor_f32_config1_geometry(gpu):
 def test_factor_delay_aligned_tiles(gpu, pad, descending, mode):
     """Delay-aligned factorised tiles (pdd_sweep.hip fx_skew): each trial's
     time tile is skewed by its delay at a mid-band reference group, here by up
-    to ~180 samples (two extra time tiles per segment), so tiles of one trial
+    to ~175 samples (two extra time tiles per segment), so tiles of one trial
     block store different column ranges and the first / last tiles store only
     part of their elements.  The plane equals the plane-aligned tiles' plane
     and the oracle's bit for bit: value / rotate pads, trim on and off, both
     band orders, a grid over two trial blocks with a partial second block."""
     import torch
     from pypulsar_amd.sweep import DMSweep
-    C, N, D = 64, 6000, 200
+    C, N, D = 256, 6000, 200
     freqs = band(C, descending=descending)
     x = u8_data(C, N, 61)
     xd = torch.from_numpy(x).cuda()

@@ -110,6 +110,9 @@ def _worker(rank, world, port, q):
             for _ in range(2):
                 out = ts(blk[lo:hi].contiguous())
             ts_res[gather] = (ts.a, out.numpy().copy())
+            # the PCIe-inclusive step (bench.py's end_to_end_pcie leg at N > 1),
+            # with and without the gather to rank 0: the same result
+            ts_res[("host", gather)] = ts.host_step(blk[lo:hi].contiguous(), n_batches=3).numpy().copy()
         tsr = [None] * world
         dist.all_gather_object(tsr, ts_res[False])
         res = {}
@@ -149,6 +152,9 @@ def _worker(rank, world, port, q):
             q.put(("sp", cands))
             q.put(("ts", np.concatenate([p for _, p in sorted(tsr, key=lambda a: a[0])], axis=1)))
             q.put(("tsg", ts_res[True][1]))
+            q.put(("tshg", ts_res[("host", True)]))
+        # every rank: host_step == __call__ (its own columns)
+        np.testing.assert_array_equal(ts_res[("host", False)], ts_res[False][1])
     finally:
         dist.destroy_process_group()
 
@@ -162,7 +168,7 @@ def test_sharded_sweeps_equal_one_shot(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=240) for _ in range(10))
+    got = dict(q.get(timeout=240) for _ in range(11))
     for p in procs:
         p.join(timeout=240)
         assert p.exitcode == 0
@@ -184,6 +190,7 @@ def test_sharded_sweeps_equal_one_shot(world):
         np.testing.assert_array_equal(got["aggp"].astype(np.float64), want_p)
     np.testing.assert_array_equal(got["ts"].astype(np.float64), want_b)
     np.testing.assert_array_equal(got["tsg"].astype(np.float64), want_b)
+    np.testing.assert_array_equal(got["tshg"].astype(np.float64), want_b)
     # sharded search == search of the one-shot plane
     from oracle import search_oracle as so
     xs = _data(C, N)
