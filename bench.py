@@ -1377,18 +1377,25 @@ def subband_bench(args, cfg, rank, world, dev):
 
 
 def subband_roofline(ex, spectra, one, steps, C, N):
-    """Per-stage HBM roofline of a chained two-stage DDplan step (configs[2]:
+    """Per-stage roofline of a chained two-stage DDplan step (configs[2]:
     pdd_subband_chain = the stage-1 interleave pre-pass (8-bit rows co-added
     by ds into u16 eighths), the stage-1 grouped sweep writing stage 2's
     float32 quarters image, the stage-2 grouped sweep writing the plane).
     The two sweep kernels are timed by their plans' HIP event pairs, the
     whole chain by events around it on the same stream; the pre-pass is the
-    remainder.  Algorithmic bytes per stage: its input once + its output
-    once."""
+    remainder.  Each stage is priced against its own bound: the pre-pass
+    against HBM (its input once + its output once), the sweeps against the
+    LDS read roof of their image (u16 eighths: 2 B per add; float32
+    quarters: 4 B per add) in the adds of the plan's REAL trials (the tile's
+    padded trial slots are not counted), with their HBM fractions beside.
+    None unless the chained u16 stage 1 ran (8-bit rows, integer pads:
+    otherwise stage 1 is a float32 sweep and its timers read 0)."""
     st = [s for s in ex.steps if s.two_stage and s.chain]
     if len(ex.steps) != 1 or not st:
         return None
     s = st[0]
+    if s.int1 != "u16":
+        return None
     i1, i2 = s.g1.info(), s.g2.info()
     n1 = N // s.ds
     tq = i1["samples_per_block"] // 8                   # u16 eighths: Tq elements
@@ -1399,8 +1406,13 @@ def subband_roofline(ex, spectra, one, steps, C, N):
     b_pre = C * N + C * nr1 * 16                         # raw 8-bit rows in, u16 eighths out
     b_s1 = C * nr1 * 16 + rows2 * nr2 * 16               # eighths in, quarters image out
     b_s2 = rows2 * nr2 * 16 + s.ncall * s.per * s.n_out * 4   # quarters in, plane out
+    cps = C // s.nsub
+    adds1 = s.nsub * s.ncall * cps * n1                  # every subband sample of every pass
+    adds2 = s.ncall * s.per * s.nsub * s.n_out           # every plane sample of every DM
     s.g1.set_timing(True)
     s.g2.set_timing(True)
+    s.g1.timing_read()
+    s.g2.timing_read()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     e0.record()
@@ -1413,24 +1425,43 @@ def subband_roofline(ex, spectra, one, steps, C, N):
     k2, l2 = s.g2.timing_read()
     s.g1.set_timing(False)
     s.g2.set_timing(False)
+    if not (l1 and l2 and k1 > 0 and k2 > 0):
+        return None
     k1, k2 = k1 / steps, k2 / steps
     pre = max(t_all - k1 - k2, 1e-6)
+    lds_u16 = N_CU * CLK_GHZ * 1e9 * LDS_B_PER_CLK / 2 / 1e12    # T adds/s, 2 B per add
+    lds_f32 = lds_u16 / 2
     stages = []
-    for name, b, t in (("k_interleave_u16_ds_v (stage-1 pre-pass: co-add + eighths)", b_pre, pre),
-                       ("k_sweep_il u16 grouped, stage 1 -> stage-2 quarters image", b_s1, k1),
-                       ("k_sweep_il f32 grouped, stage 2 -> plane", b_s2, k2)):
+    for name, b, t, adds, roof, db in (
+            ("k_interleave_u16_ds_v (stage-1 pre-pass: co-add + eighths)", b_pre, pre, None,
+             None, None),
+            ("k_sweep_il u16 grouped, stage 1 -> stage-2 quarters image", b_s1, k1, adds1,
+             lds_u16, i1["dms_per_block"]),
+            ("k_sweep_il f32 grouped, stage 2 -> plane", b_s2, k2, adds2, lds_f32,
+             i2["dms_per_block"])):
         gbs = b / (t * 1e-3) / 1e9
-        stages.append({"kernel": name, "ms": t, "bytes": b, "achieved_GBs": gbs,
-                       "frac": gbs / PEAK_HBM_GBS})
-    tot = b_pre + b_s1 + b_s2
-    return {"bound": "hbm", "achieved": tot / (t_all * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
-            "unit": "GB/s", "frac": tot / (t_all * 1e-3) / 1e9 / PEAK_HBM_GBS, "traffic": None,
+        e = {"kernel": name, "ms": t, "bytes": b, "achieved_GBs": gbs,
+             "hbm_frac": gbs / PEAK_HBM_GBS}
+        if adds is None:
+            e.update(bound="hbm", frac=gbs / PEAK_HBM_GBS)
+        else:
+            ta = adds / (t * 1e-3) / 1e12
+            trials = s.ncall if "stage 1" in name else s.per
+            e.update(bound="lds", adds=adds, achieved_Tadds=ta, lds_peak_Tadds=roof,
+                     frac=ta / roof, trials_per_group=trials, tile_trials=db,
+                     tile_fill=trials / (-(-trials // db) * db))
+        stages.append(e)
+    dom = max(stages, key=lambda e: e["ms"])
+    return {"bound": dom["bound"], "achieved": dom.get("achieved_Tadds", dom["achieved_GBs"]),
+            "peak": dom.get("lds_peak_Tadds", PEAK_HBM_GBS),
+            "unit": "T adds/s" if dom["bound"] == "lds" else "GB/s",
+            "frac": dom["frac"], "kernel": dom["kernel"], "traffic": None,
             "stages": stages, "launches": [l1 // steps, l2 // steps],
-            "note": "per-stage algorithmic bytes (each stage's input once + output once) over "
-                    "its own time: the sweeps by their HIP event pairs, the pre-pass as the "
-                    "remainder of the chain's events; the stage-1 sweep's adds per byte make it "
-                    "LDS-bound rather than HBM-bound (DESIGN.md §4)"}
-
+            "chain_ms": t_all,
+            "note": "top level = the longest stage against its own bound; each stage: the "
+                    "pre-pass against HBM (input once + output once), the sweeps against the "
+                    "LDS read roof of their image in the adds of the real trials (padded tile "
+                    "slots excluded, tile_fill), with their HBM fractions (hbm_frac)"}
 
 if __name__ == "__main__":
     main()

@@ -1138,6 +1138,9 @@ __device__ __forceinline__ uint32_t add3_u32(uint32_t a, uint32_t b, uint32_t c)
 // pattern row | window count << 20}, one vector load per loader lane, two
 // chunks ahead.
 constexpr int kFxWin = 64;
+#ifndef PDD_CW_PRIO
+#define PDD_CW_PRIO 0
+#endif
 template <int G, int DPW, int NCW, int NLW, int CC, int NBUF, bool U16 = false, bool FX = false>
 __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const float4* __restrict__ R0, int64_t nR, int C, int lo, const int* __restrict__ mt,
@@ -1265,9 +1268,6 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     int4 rec_next2 = fx_rec(1);
     int rec_tail = 0;  // a record load issued after the last chunk's DMAs
     auto issue_samples = [&](int k) -> int {
-#ifdef PDD_SWEEP_DEV
-      if (dbg & 1) return 0;  // (developer builds, timing only: no window staging)
-#endif
       if constexpr (FX) {
         const int4 rec = rec_next;
         rec_next = rec_next2;  // (chunk k + 2's record: rec_ahead)
@@ -1444,6 +1444,22 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   typedef __attribute__((address_space(3))) u32x4_t lds_u32x4_t;
   uint64_t ts_poll = 0, ts_comp = 0, tA = 0, tB = 0;
   int vmeta_n = 0, ncc_n = 0;  // FX: the next chunk's shifts and count
+  // compute-wave issue priority (PDD_CW_PRIO, tuning experiments): 1 =
+  // static by age (the youngest third highest), 2 = only the youngest third
+  // raised, 3 = rotating by chunk
+  auto cw_prio = [&](int k) {
+    const int a = (w * 3) / NCW;  // 0 oldest .. 2 youngest
+    int p = 0;
+    if constexpr (PDD_CW_PRIO == 1) p = a;
+    else if constexpr (PDD_CW_PRIO == 2) p = a == 2;
+    else if constexpr (PDD_CW_PRIO == 3) p = (a + k) % 3;
+    if constexpr (PDD_CW_PRIO != 0) {
+      if (p == 0) __builtin_amdgcn_s_setprio(0);
+      else if (p == 1) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(2);
+    }
+  };
+  cw_prio(0);
   __builtin_amdgcn_s_barrier();  // prologue barrier (metadata landed)
   asm volatile("" ::: "memory");
   if (stamps) tB = __builtin_amdgcn_s_memtime();
@@ -1455,6 +1471,7 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if constexpr (PDD_CW_PRIO == 3) cw_prio(k);
     if (stamps) { tB = __builtin_amdgcn_s_memtime(); ts_poll += tB - tA; }
     const int slot = k % MR;
     // ONE ds_read_b32 brings the wave's DPW shifts of all CC channels of the
@@ -1491,9 +1508,6 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
       ncc = __builtin_amdgcn_readfirstlane(read_count(slot)) >> 20;
     }
     const uint32_t cb = lane_byte + (uint32_t)(b * buf_e * 16);
-#ifdef PDD_SWEEP_DEV
-    if (dbg & 2) continue;  // (developer builds, timing only: no reads / adds)
-#endif
     if constexpr (U16) {
       // normalise before a chunk could carry a u16 lane past 65535
       if (since_flush + ncc > flush_n) {
@@ -1681,9 +1695,6 @@ static const Variant kU8Variants[] = {
     {0, false, 4, 4, 4, 8, 8, 2, 2},    // f32 image of u8 data, DB 32
     {1, true, 8, 2, 1, 8, 1, 2, 0},     // generic u16, DB 8
     {1, true, 8, 1, 1, 1, 1, 2, 0}      // generic u16, DB 1
-#ifdef PDD_SWEEP_DEV
-    , {0, false, 8, 2, 5, 12, 8, 2, 4}  // dev (PDD_SWEEP_VARIANT=5): u16 eighths, DB 60
-#endif
 };
 
 // LDS per workgroup: 16-wave (il) tiles run one per CU, <= 8-wave tiles two
@@ -1704,9 +1715,6 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false) {
       if (v.DPW == 8) return k_sweep_il<2, 8, 12, 4, 8, 2, true, true>;
       if (v.DPW == 6) return k_sweep_il<2, 6, 12, 4, 8, 2, true, true>;
       if (v.DPW == 4) return k_sweep_il<2, 4, 12, 4, 8, 2, true, true>;
-#ifdef PDD_SWEEP_DEV
-      if (v.DPW == 5) return k_sweep_il<2, 5, 12, 4, 8, 2, true, true>;
-#endif
     }
     if (v.S == 4 && v.NW == 14 && v.NLW == 2 && v.G == 4 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2)
       return k_sweep_il<4, 4, 14, 2, 8, 2, false, true>;
@@ -1715,9 +1723,6 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false) {
   if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.CC == 8 && v.NBUF == 2) {
     if (v.DPW == 6) return k_sweep_il<2, 6, 12, 4, 8, 2, true>;
     if (v.DPW == 4) return k_sweep_il<2, 4, 12, 4, 8, 2, true>;
-#ifdef PDD_SWEEP_DEV
-    if (v.DPW == 5) return k_sweep_il<2, 5, 12, 4, 8, 2, true>;
-#endif
   }
   if (v.S == 4 && v.G == 4 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2) {
     if (v.NW == 14 && v.NLW == 2) return k_sweep_il<4, 4, 14, 2, 8, 2>;
@@ -1743,27 +1748,12 @@ static sweep_fn kernel_for(const Variant& v) {
   return nullptr;
 }
 
-// Developer knobs, compiled only into developer builds (-DPDD_SWEEP_DEV,
-// scripts/build_dev.sh): PDD_SWEEP_DEBUG bit 2 writes per-wave cycle stamps
-// instead of the plane (scripts/probes/il_stamps.py); bits 0 / 1 (timing
-// only, wrong planes) drop the loaders' window DMAs / the compute waves'
-// reads and adds (k_sweep_il), the time decomposition of DESIGN.md §3;
-// PDD_SWEEP_VARIANT
-// forces a candidate tiling by index.  Production builds read no
-// environment variable.
-#ifdef PDD_SWEEP_DEV
-static int debug_flags() {
-  const char* e = getenv("PDD_SWEEP_DEBUG");
-  return e ? atoi(e) : 0;
-}
-static int forced_variant() {
-  const char* e = getenv("PDD_SWEEP_VARIANT");
-  return e ? atoi(e) : -1;
-}
-#else
+// Developer knobs (kernel stamps, timing-only decompositions, forced
+// tilings) live in scripts/probes/dev_knobs.patch, applied to a copy of this
+// file by scripts/build_dev.sh; the production library reads no environment
+// variable: no debug bits, no forced tiling.
 static int debug_flags() { return 0; }
 static int forced_variant() { return -1; }
-#endif
 
 }  // namespace pdd
 
@@ -2530,11 +2520,6 @@ static bool fx_build(const int32_t* tab, int64_t D, int64_t C, const Variant& v,
   // modelled cost: configs[1] u8 g 2 models at 0.927 and measures 18.6
   // against 21.6 ms per step; the margin was 0.9.  Developer builds print the
   // model's numbers with PDD_SWEEP_DEBUG bit 3.)
-#ifdef PDD_SWEEP_DEV
-  if (debug_flags() & 8)
-    fprintf(stderr, "fx_build g %d DB %lld buf %lld: n_pat %lld cost_f %.3g cost_b %.3g el_f %.3g el_b %.3g pairs %d ratio %.3f\n",
-            fx, (long long)DB, (long long)buf_e, (long long)T.n_pat, cost_f, cost_b, T.el_f, T.el_b, (int)pairs, T.pair_ratio);
-#endif
   if (!force && cost_f > 0.95 * cost_b) return false;
   T.rows_pb = rows_pb;
   T.mt.assign((size_t)(n_dblk * rows_pb * ROW), 0);
@@ -2600,7 +2585,15 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
                            : (int)(sizeof(kF32Variants) / sizeof(Variant));
 
   const int fv = forced_variant();
-  for (int vi = (fv >= 0 && fv < ncand) ? fv : 0; vi < ncand; ++vi) {
+  // Short grids (the grouped sweeps of a DDplan step: 40-50 trials per
+  // group) waste most of a 72-trial tile: 8/16-bit plans start at the
+  // 48-trial tiling when it pads the grid to >= 3% fewer trial slots
+  // (configs[2] stage 1: 40 trials in 48 slots instead of 72)
+  int v0 = 0;
+  if (int_in && cdiv(D, (int64_t)kU8Variants[1].DB()) * kU8Variants[1].DB() * 103 <
+                    cdiv(D, (int64_t)kU8Variants[0].DB()) * kU8Variants[0].DB() * 100)
+    v0 = 1;
+  for (int vi = (fv >= 0 && fv < ncand) ? fv : v0; vi < ncand; ++vi) {
     const Variant v = cands[vi];
     const bool il = v.kind == 0;
     if (n_grp > 1 && !il) continue;  // only the interleaved kernel sweeps groups
