@@ -154,7 +154,7 @@ def _pinned_h2d_GBs(h, dev, reps=5):
     return h.numel() * h.element_size() / best / 1e9
 
 
-def stream_cpu_baseline(C, ds, dms, dt, nb_gpu, D, mode, n_raw=1 << 15, ntrials=6):
+def stream_cpu_baseline(C, ds, dms, dt, nb_gpu, D, mode, n_raw=1 << 17, ntrials=12):
     """The stream's per-block work on the host: the oracle's
     zero-DM (the reference's uint8 result, bin/zero_dm_filter.py:30-39, per
     spectrum) + downsample (formats/spectra.py:329-351) of an ``n_raw``-
@@ -172,6 +172,7 @@ def stream_cpu_baseline(C, ds, dms, dt, nb_gpu, D, mode, n_raw=1 << 15, ntrials=
         z = orc.zdm_downsample(x, ds, zero_dm=True)
     else:
         z = orc.zdm_int_downsample(x, ds, mode=zmode).astype(np.float64)
+    z = np.ascontiguousarray(z)  # [C, n] channel rows, C-order (as Spectra.data)
     t_pro = time.perf_counter() - t0
     pick = dms[np.linspace(0, len(dms) - 1, ntrials).astype(int)]
     cols, t0 = [], time.perf_counter()
@@ -1222,7 +1223,6 @@ def stream_bench(args, cfg, rank, world, dev):
             # the sweep kernel's own launches, timed by the plan's HIP event
             # pairs on the stream it runs on (its LDS fraction below)
             st.sweep.set_timing(True, code=_lib.U16 if st.exact else _lib.F32)
-            st.sweep.timing_read()
             t0 = time.perf_counter()
         if done == args.warmup + args.steps:
             break
@@ -1411,8 +1411,6 @@ def subband_roofline(ex, spectra, one, steps, C, N):
     adds2 = s.ncall * s.per * s.nsub * s.n_out           # every plane sample of every DM
     s.g1.set_timing(True)
     s.g2.set_timing(True)
-    s.g1.timing_read()
-    s.g2.timing_read()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     e0.record()

@@ -21,9 +21,20 @@ int main(int argc, char** argv) {
     for (int pairs = 1; pairs >= 0; --pairs) {
       FxTables T;
       const bool ok = fx_build(tab.data(), D, C, v, buf, g, true, T, pairs, skew);
-      int64_t nch = 0;
+      int64_t nch = 0, nwin = 0, el = 0;
       const int64_t nb = cdiv(D, v.DB());
       for (int64_t b = 0; b < nb; ++b) nch += ok ? T.cht[(size_t)(b * (T.maxch + 1))] : 0;
+      for (int64_t b = 0; ok && b < nb; ++b)
+        for (int k = 0; k < T.cht[(size_t)(b * (T.maxch + 1))]; ++k)
+          for (int i = 0; i < kFxWin; ++i) {
+            const int* r = &T.wt[(((size_t)b * T.maxch + k) * kFxWin + i) * 4];
+            if (r[1] == 0 || (r[3] & 0xfffff) == T.n_pat) continue;  // empty / pad group
+            ++nwin;
+            el += r[1];
+          }
+      if (ok)
+        printf("  windows per (block, group) %.2f, mean window %.1f elements (Tq %d + span %.1f)\n",
+               (double)nwin / (nb * (C / g)), (double)el / nwin, 64 * v.G, (double)el / nwin - 64 * v.G);
       printf("skew %d pairs %d ok %d: n_pat %lld cost_f %.4g cost_b %.4g el_f/tile %.4g chunks/blk %.1f "
              "pair_ratio %.5f sig_max %d lo %d hi %d\n",
              skew, pairs, (int)ok, (long long)T.n_pat, T.cost_f, T.cost_b, T.el_f, (double)nch / nb,

@@ -262,3 +262,49 @@ def test_factor_delay_aligned_tiles(gpu, pad, descending, mode):
                                       err_msg="pad %r trim %s" % (pad, trim))
     sk.close()
     al.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["u8_const255", "u16_const1023", "u8_extremes"])
+def test_factor_saturated_accumulators(gpu, case):
+    """The packed-u16 accumulation at its limits (k_sweep_il normalise16 /
+    HI8 carry bytes): plane sums up to 255 * 2^15 (the plan's HI8 bound,
+    C * input bound <= 255 * 32768), lanes flushed every floor(32767 / (g x
+    bound)) groups.
+      u8_const255: 32 768 channels of 255 -- every sum 255 * C = 8 355 840, the
+        carry bytes at 255;
+      u16_const1023: 8164 channels of 1023 (groups of 4: flush every 8
+        groups, = the chunk's group count) -- sums 8 351 772;
+      u8_extremes: random 0 / 255 samples on 32 768 channels -- the factorised
+        plane equals the channel-by-channel kernel's (u16 carries, DB 72)."""
+    import torch
+    from pypulsar_amd import _lib
+    from pypulsar_amd.sweep import DMSweep
+    N, D = 4096, 96
+    if case == "u16_const1023":
+        C, dtype, code, v = 8164, "u16", _lib.U16, 1023
+    else:
+        C, dtype, code, v = 32768, "u8", _lib.U8, 255
+    freqs = band(C)
+    dms = np.linspace(0.0, 2.0, D)
+    if case == "u8_extremes":
+        g = torch.Generator(device="cuda")
+        g.manual_seed(9)
+        x = (torch.randint(0, 2, (C, N), generator=g, device="cuda", dtype=torch.uint8) * 255)
+    elif dtype == "u8":
+        x = torch.full((C, N), v, dtype=torch.uint8, device="cuda")
+    else:
+        x = torch.full((C, N), v, dtype=torch.int16, device="cuda")
+    sw = DMSweep(dms, freqs, DT, dtype=dtype, factor="force4")
+    assert sw.factor_info(code)[0] == 4
+    plane = sw(x)
+    assert plane.shape[1] > 2048
+    if case == "u8_extremes":
+        ch = DMSweep(dms, freqs, DT, dtype=dtype, factor=False)
+        assert ch.factor_info(code)[0] == 0
+        assert torch.equal(plane, ch(x))
+        ch.close()
+    else:
+        assert 255 * 32768 - 4 * 1023 <= v * C <= 255 * 32768
+        assert torch.all(plane == float(v * C)), (plane.min().item(), plane.max().item())
+    sw.close()
