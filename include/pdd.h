@@ -239,6 +239,24 @@ int pdd_sweep_execute_ex(const pdd_sweep_plan* plan, const void* x, int64_t N, i
                          int64_t piece, int64_t x_off, int pad_mode, const float* padvals,
                          float* out, int64_t ld_out, int64_t n_out, float out_bias,
                          void* stream);
+/* Staged execution of a factorised plan (pdd_sweep_plan_factor > 0, raw-rate
+ * input) for pipelining: stage 1 (1: the pattern image, written into
+ * `patterns`), stage 2 (2: the sweep, reading the pattern image stage 1 of the
+ * same x / x_off / n_out wrote into `patterns`) or both (3), one segment (the
+ * whole column range) per call, arguments as pdd_sweep_execute_ex.  Two
+ * pattern buffers let stage 1 of the next block run on one stream while
+ * stage 2 of this block runs on another (DMShardedSweep: CU-partitioned
+ * streams, pdd_stream_create_cu_mask).  `pattern_bytes` must be >=
+ * pdd_sweep_pattern_bytes(plan, n_out). */
+int64_t pdd_sweep_pattern_bytes(const pdd_sweep_plan* plan, int64_t n_out);
+int pdd_sweep_execute_stage(const pdd_sweep_plan* plan, const void* x, int64_t N, int64_t ld,
+                            int64_t piece, int64_t x_off, int pad_mode, const float* padvals,
+                            float* out, int64_t ld_out, int64_t n_out, float out_bias,
+                            void* patterns, int64_t pattern_bytes, int stage, void* stream);
+/* A stream whose kernels run only on the CUs set in `mask` (n_words 32-bit
+ * words, bit i = CU i; hipExtStreamCreateWithCUMask) / its release. */
+int pdd_stream_create_cu_mask(const uint32_t* mask, int n_words, void** stream);
+int pdd_stream_destroy(void* stream);
 /* Grouped sweep: n_grp independent channel groups of C channels each
  * (channels g*C .. g*C+C-1 of the input), every group with its own [D][C]
  * table: host_table is [n_grp][D][C].  One launch replaces n_grp sweeps --

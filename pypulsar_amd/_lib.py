@@ -49,6 +49,8 @@ EXPORTS = (
     "pdd_sweep_execute_ds", "pdd_subband_chain", "pdd_scratch_release",
     "pdd_sweep_plan_create_ex", "pdd_sweep_plan_factor", "pdd_sweep_plan_skew", "pdd_source_digest",
     "pdd_sweep_plan_set_poison", "pdd_sweep_plan_set_segment_bytes",
+    "pdd_sweep_pattern_bytes", "pdd_sweep_execute_stage", "pdd_stream_create_cu_mask",
+    "pdd_stream_destroy",
 )
 
 
@@ -95,6 +97,11 @@ _SIGS = {
     "pdd_sweep_execute_ex": ([_vp, _vp, _i64, _i64, _i64, _i64, _int, _vp, _vp, _i64, _i64,
                               ctypes.c_float, _vp], _int),
     "pdd_sweep_plan_info": ([_vp, _vp], _int),
+    "pdd_sweep_pattern_bytes": ([_vp, _i64], _i64),
+    "pdd_sweep_execute_stage": ([_vp, _vp, _i64, _i64, _i64, _i64, _int, _vp, _vp, _i64, _i64,
+                                 ctypes.c_float, _vp, _i64, _int, _vp], _int),
+    "pdd_stream_create_cu_mask": ([_vp, _int, ctypes.POINTER(_vp)], _int),
+    "pdd_stream_destroy": ([_vp], _int),
     "pdd_sweep_plan_set_input_max": ([_vp, _int], _int),
     "pdd_sweep_plan_destroy": ([_vp], _int),
     "pdd_global_stats": ([_vp, _i64, _i64, _i64, _vp, _vp], _int),

@@ -1860,6 +1860,12 @@ struct IlExtra {
   int64_t r2_nR = 0, r2_ov = 0;
   const float4* R_pre = nullptr;
   int64_t Qs_pre = 0, nR_pre = 0;
+  // factorised plans, staged execution (pdd_sweep_execute_stage): bit 0 =
+  // stage 1 (pattern image), bit 1 = stage 2 (the sweep), into the caller's
+  // pattern buffer P_ext of P_bytes (one segment)
+  int stages = 3;
+  uint4* P_ext = nullptr;
+  int64_t P_bytes = 0;
 };
 static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayout lay,
                       int64_t x_off, int pad_mode, const float* padvals, float* out,
@@ -1882,7 +1888,8 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
   int64_t lo, hi;
   il_lohi(p, lo, hi);
   // output samples per segment
-  int64_t seg = ex.one_seg ? std::max<int64_t>(n_out, 1) : il_seg_samples(p, as_stream(stream));
+  int64_t seg = (ex.one_seg || ex.P_ext) ? std::max<int64_t>(n_out, 1)
+                                         : il_seg_samples(p, as_stream(stream));
   PDD_REQUIRE(seg > 0, "pdd_sweep_execute: delay span %lld too wide for the segment budget",
               (long long)(hi - lo));
   // equal segments (whole tiles): every launch does the same work
@@ -1909,13 +1916,20 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
   }
   // factorised plans: the pattern image (stage 1), n_pat rows + a row of zeros
   uint4* P = nullptr;
+  if (ex.P_ext) {
+    PDD_REQUIRE(p->fx && (int64_t)(p->n_pat + 1) * nr_alloc * 16 <= ex.P_bytes,
+                "pdd_sweep_execute_stage: pattern buffer of %lld bytes < %lld",
+                (long long)ex.P_bytes, (long long)((p->n_pat + 1) * nr_alloc * 16));
+    P = ex.P_ext;
+  }
   if (p->fx) {
     // (ds > 1: the interleave pre-pass co-adds the raw rows into R and stage
     // 1 builds the patterns from R: sums of fx co-adds <= 4 * 1020 stay exact)
     PDD_REQUIRE(u16 == (p->dtype != PDD_F32) && !ex.r2_pad && !ex.R_pre && p->n_grp == 1 &&
                     (u16 || fx_direct),
                 "pdd_sweep_execute: factorised plans take single-group input (float32: raw rate)");
-    P = static_cast<uint4*>(scratch(st, kScratchPattern, (size_t)((p->n_pat + 1) * nr_alloc) * sizeof(uint4)));
+    if (!P)
+      P = static_cast<uint4*>(scratch(st, kScratchPattern, (size_t)((p->n_pat + 1) * nr_alloc) * sizeof(uint4)));
     if (!P) return -2;
   }
   const int dbg = debug_flags();
@@ -1969,7 +1983,7 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
       hipLaunchKernelGGL(k_interleave<float>, g1, dim3(256), 0, st, (const float*)x, lay, N,
                          t_base + lo + x_off, Qs, nR, pad_mode, padvals, R);
     if (hipGetLastError() != hipSuccess) { rc = -3; break; }
-    if (p->fx) {
+    if (p->fx && (ex.stages & 1)) {
       // pdd_sweep_plan_set_poison (a parity-test switch): the pattern rows
       // are filled with 0xFF bytes first, so a sum that read an element stage
       // 1 did not write (the per-pattern ranges of fx_build) shows as a NaN /
@@ -2016,6 +2030,7 @@ static int execute_il(const pdd_sweep_plan* p, const void* x, int64_t N, InLayou
     }
     // (delay-aligned factorised tiles: fx_tpad / Tq more time tiles, whose
     // trials cover the columns their skew moved past the last tile)
+    if (!(ex.stages & 2)) continue;  // (staged: stage 1 only)
     const int64_t n_tblk = Qs / Tq + (p->fx ? p->fx_tpad / Tq : 0);
     const int64_t blocks = n_tblk * p->n_dblk * p->n_grp;
     if (blocks >= (1ll << 31)) { rc = -1; break; }
@@ -2929,6 +2944,58 @@ int pdd_sweep_execute_ex(const pdd_sweep_plan* p, const void* x, int64_t N, int6
                      p->d_bmin, p->d_bspan, pad_mode, padvals, out, ld_out, n_out, debug_flags(),
                      p->stride, (int)n_tblk, (int)p->n_dblk);
   PDD_LAUNCHED();
+  return 0;
+}
+
+int64_t pdd_sweep_pattern_bytes(const pdd_sweep_plan* p, int64_t n_out) {
+  PDD_REQUIRE(p && n_out >= 0, "pdd_sweep_pattern_bytes: bad arguments");
+  if (!p->fx || !p->d_gtab || p->v.kind != 0) return 0;
+  const int Tq = 64 * p->v.G;
+  int64_t lo, hi;
+  il_lohi(p, lo, hi);
+  const int64_t Qs = cdiv(cdiv(std::max<int64_t>(n_out, 1), p->v.S), Tq) * Tq;
+  return (int64_t)(p->n_pat + 1) * (Qs + (hi - lo) + 64) * 16;
+}
+
+int pdd_sweep_execute_stage(const pdd_sweep_plan* p, const void* x, int64_t N, int64_t ld,
+                            int64_t piece, int64_t x_off, int pad_mode, const float* padvals,
+                            float* out, int64_t ld_out, int64_t n_out, float out_bias,
+                            void* patterns, int64_t pattern_bytes, int stage, void* stream) {
+  PDD_REQUIRE(p && x && patterns && (out || stage == 1), "pdd_sweep_execute_stage: null pointer");
+  PDD_REQUIRE(p->fx && p->d_gtab && p->v.kind == 0 && p->n_grp == 1,
+              "pdd_sweep_execute_stage: needs a factorised single-group plan");
+  PDD_REQUIRE(stage >= 1 && stage <= 3, "pdd_sweep_execute_stage: stage %d not 1, 2 or 3", stage);
+  PDD_REQUIRE(N > 0 && n_out >= 0 && (stage == 1 || ld_out >= n_out) && x_off >= 0,
+              "pdd_sweep_execute_stage: bad shape");
+  PDD_REQUIRE(piece > 0 || ld >= N, "pdd_sweep_execute_stage: row stride %lld < N", (long long)ld);
+  PDD_REQUIRE(piece == 0 || (piece & (piece - 1)) == 0, "pdd_sweep_execute_stage: piece must be 2^k");
+  PDD_REQUIRE(pad_mode == PDD_PAD_ROTATE || (pad_mode == PDD_PAD_VALUE && padvals),
+              "pdd_sweep_execute_stage: bad pad mode %d", pad_mode);
+  if (n_out == 0) return 0;
+  InLayout lay{ld, piece, 0, 0};
+  if (piece) {
+    while ((1ll << lay.psh) < piece) ++lay.psh;
+    lay.pstride = p->C * piece;
+  }
+  IlExtra ex;
+  ex.stages = stage;
+  ex.P_ext = static_cast<uint4*>(patterns);
+  ex.P_bytes = pattern_bytes;
+  return execute_il(p, x, N, lay, x_off, pad_mode, padvals, out, ld_out, n_out, 0, 1, out_bias,
+                    stream, ex);
+}
+
+int pdd_stream_create_cu_mask(const uint32_t* mask, int n_words, void** stream) {
+  PDD_REQUIRE(mask && stream && n_words > 0, "pdd_stream_create_cu_mask: bad arguments");
+  hipStream_t st = nullptr;
+  PDD_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)n_words, mask));
+  *stream = st;
+  return 0;
+}
+
+int pdd_stream_destroy(void* stream) {
+  PDD_REQUIRE(stream, "pdd_stream_destroy: null stream");
+  PDD_HIP(hipStreamDestroy(as_stream(stream)));
   return 0;
 }
 

@@ -285,6 +285,33 @@ class DMSweep(object):
              ptr(pv), ptr(out), out.stride(0), n_out, 0.0, stream_ptr(stream))
         return out
 
+    def pattern_bytes(self, n_out, code=_lib.U8):
+        """Bytes of the pattern image one staged launch of ``n_out`` columns
+        needs (0: not a factorised plan; pdd_sweep_pattern_bytes)."""
+        return int(_lib.lib().pdd_sweep_pattern_bytes(self._plan(code), int(n_out)))
+
+    def sweep_pieces_stage(self, xp, N, piece, x_off, n_out, out, patterns, stage, stream=None):
+        """Stage 1 (the pattern image into ``patterns``, a uint8 device
+        buffer of >= pattern_bytes(n_out)), stage 2 (the sweep of that image
+        into ``out``) or both (3) of sweep_pieces on a factorised plan
+        (pdd_sweep_execute_stage): stage 1 of the next block can run on one
+        stream while stage 2 of this one runs on another."""
+        code = _lib.U8 if xp.dtype == torch.uint8 else _lib.F32
+        assert out is None or (out.shape[0] == self.D and out.shape[1] >= n_out
+                               and out.stride(1) == 1)
+        assert patterns.is_cuda and patterns.is_contiguous()
+        nbytes = patterns.numel() * patterns.element_size()
+        # (the zero pads are allocated once: a fill kernel on torch's default
+        # stream would serialise the CU-partitioned streams of a pipeline)
+        pv = getattr(self, "_pv0", None)
+        if pv is None or pv.device != xp.device:
+            pv = self._pv0 = torch.zeros(self.C, dtype=torch.float32, device=xp.device)
+        ld = 0 if piece else xp.stride(0)  # piece 0: channel-major [C][ld] rows
+        call("pdd_sweep_execute_stage", self._plan(code), ptr(xp), N, ld, piece, x_off,
+             _lib.PAD_VALUE, ptr(pv), ptr(out), out.stride(0) if out is not None else 0, n_out,
+             0.0, ptr(patterns), nbytes, int(stage), stream_ptr(stream))
+        return out
+
     def set_timing(self, on=True, code=None):
         """Bracket the sweep kernel of every execute with HIP events (on the
         execute stream); read the last duration with kernel_ms()."""
@@ -628,3 +655,29 @@ def execute_plan_grouped(spectra, ddplan, padval=0):
     out = ex(spectra, padval=padval)
     ex.close()
     return out
+
+
+def cu_masked_stream(cus, device=None):
+    """A torch ExternalStream whose kernels run only on the compute units in
+    ``cus`` (pdd_stream_create_cu_mask / hipExtStreamCreateWithCUMask); the
+    HIP stream lives until cu_stream_release(stream)."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    n = max(cus) // 32 + 1
+    words = np.zeros(max(n, 8), dtype=np.uint32)
+    for c in cus:
+        words[c // 32] |= np.uint32(1 << (c % 32))
+    h = ctypes.c_void_p()
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().pdd_stream_create_cu_mask(words.ctypes.data_as(ctypes.c_void_p),
+                                                        len(words), ctypes.byref(h)),
+                   "pdd_stream_create_cu_mask")
+        st = torch.cuda.ExternalStream(h.value, device=dev)
+    st._pdd_handle = h
+    return st
+
+
+def cu_stream_release(st):
+    h = getattr(st, "_pdd_handle", None)
+    if h is not None and h.value:
+        _lib.check(_lib.lib().pdd_stream_destroy(h), "pdd_stream_destroy")
+        st._pdd_handle = None

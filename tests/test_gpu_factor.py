@@ -308,3 +308,51 @@ def test_factor_saturated_accumulators(gpu, case):
         assert 255 * 32768 - 4 * 1023 <= v * C <= 255 * 32768
         assert torch.all(plane == float(v * C)), (plane.min().item(), plane.max().item())
     sw.close()
+
+
+@pytest.mark.gpu
+def test_factor_staged_execution_on_cu_partitioned_streams(gpu):
+    """pdd_sweep_execute_stage: stage 1 of block k+1 into one pattern buffer
+    on a stream of 32 CUs while stage 2 of block k reads the other buffer on
+    a stream of the remaining CUs (pdd_stream_create_cu_mask): every plane
+    equals the one-shot factorised sweep (stage 3) and the channel kernel."""
+    import torch
+    from pypulsar_amd.sweep import DMSweep, cu_masked_stream, cu_stream_release
+    C, N, D = 1024, 1 << 16, 512
+    freqs = band(C)
+    dms = np.linspace(0, 500, D)
+    sw = DMSweep(dms, freqs, DT, dtype="u8", factor="force")
+    assert sw.factor_info()[0] == 4
+    plain = DMSweep(dms, freqs, DT, dtype="u8", factor=False)
+    n_out = sw.n_out(N)
+    xs = [torch.from_numpy(u8_data(C, N, 70 + k)).cuda() for k in range(3)]
+    refs = [plain(x) for x in xs]
+    nb = sw.pattern_bytes(n_out)
+    assert nb > 0 and plain.pattern_bytes(n_out) == 0
+    bufs = [torch.empty(nb, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    outs = [torch.full((D, n_out), -1.0, device="cuda") for _ in range(3)]
+    s1 = cu_masked_stream(range(224, 256))
+    s2 = cu_masked_stream(range(224))
+    done1 = [torch.cuda.Event() for _ in range(3)]
+    done2 = [torch.cuda.Event() for _ in range(3)]
+    torch.cuda.synchronize()
+    for k in range(3):
+        if k >= 2:
+            s1.wait_event(done2[k - 2])  # buffer k % 2 is free once stage 2 of k - 2 ran
+        sw.sweep_pieces_stage(xs[k], N, 0, 0, n_out, None, bufs[k % 2], 1, stream=s1)
+        done1[k].record(s1)
+        s2.wait_event(done1[k])
+        sw.sweep_pieces_stage(xs[k], N, 0, 0, n_out, outs[k], bufs[k % 2], 2, stream=s2)
+        done2[k].record(s2)
+    torch.cuda.synchronize()
+    for k in range(3):
+        assert torch.equal(outs[k], refs[k]), k
+    one = torch.empty_like(outs[0])
+    sw.sweep_pieces_stage(xs[0], N, 0, 0, n_out, one, bufs[0], 3)
+    assert torch.equal(one, refs[0])
+    with pytest.raises(Exception):
+        sw.sweep_pieces_stage(xs[0], N, 0, 0, n_out, one, bufs[0][: nb // 2], 2)
+    cu_stream_release(s1)
+    cu_stream_release(s2)
+    sw.close()
+    plain.close()
