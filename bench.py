@@ -817,6 +817,7 @@ def rehearse_bench(args, cfg, dev):
                          device=dev, factor=_factor_arg(args))
     t1, k1, l1 = timed(ds1, block.view(1, N, C))
     db = ds1.sw.info(1 if dtype == "u8" else 0)["dms_per_block"]
+    fx1 = ds1.sw.factor_info(1 if dtype == "u8" else 0)
     ds1.close()
     del ds1
     torch.cuda.empty_cache()
@@ -831,9 +832,15 @@ def rehearse_bench(args, cfg, dev):
         part = split_block(block, nb, W, r)
         t, k, l = timed(ds, part)
         blocks = -(-ds.rows // db)
+        code = 1 if dtype == "u8" else 0
+        g, npat = ds.sw.factor_info(code)
+        # stage 1's pattern image of the rank's slice (bytes written per batch)
+        pbytes = ds.sw.pattern_bytes(max(ds.col_edges[1] - ds.col_edges[0], 1), code) if g else 0
         ranks.append({"rank": r, "dms": [ds.lo, ds.hi], "rows": ds.rows, "step_ms": t,
                       "sweep_kernel_ms": k, "launches": l, "trial_blocks": blocks,
-                      "trial_block_fill": ds.rows / (blocks * db)})
+                      "trial_block_fill": ds.rows / (blocks * db),
+                      "outside_stage2_ms": t - k, "fx": [g, npat],
+                      "pattern_bytes_per_batch": pbytes})
         log("rehearse: rank %d/%d DMs [%d, %d) step %.1f ms (sweep %.1f ms)"
             % (r, W, ds.lo, ds.hi, t, k))
         ds.close()
@@ -850,7 +857,8 @@ def rehearse_bench(args, cfg, dev):
                                % (C, int(np.log2(N)), D, cfg["dm_lo"], cfg["dm_hi"], nb,
                                   N // (nb * W)),
                    "config_name": args.config, "dms_per_trial_block": db},
-        "one_gpu": {"step_ms": t1, "sweep_kernel_ms": k1, "launches": l1},
+        "one_gpu": {"step_ms": t1, "sweep_kernel_ms": k1, "launches": l1,
+                    "outside_stage2_ms": t1 - k1, "fx": list(fx1)},
         "ranks": ranks,
         "max_rank_step_ms": tmax,
         "mean_rank_step_ms": float(np.mean([x["step_ms"] for x in ranks])),
