@@ -1138,9 +1138,6 @@ __device__ __forceinline__ uint32_t add3_u32(uint32_t a, uint32_t b, uint32_t c)
 // pattern row | window count << 20}, one vector load per loader lane, two
 // chunks ahead.
 constexpr int kFxWin = 64;
-#ifndef PDD_CW_PRIO
-#define PDD_CW_PRIO 0
-#endif
 template <int G, int DPW, int NCW, int NLW, int CC, int NBUF, bool U16 = false, bool FX = false>
 __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     const float4* __restrict__ R0, int64_t nR, int C, int lo, const int* __restrict__ mt,
@@ -1444,22 +1441,11 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
   typedef __attribute__((address_space(3))) u32x4_t lds_u32x4_t;
   uint64_t ts_poll = 0, ts_comp = 0, tA = 0, tB = 0;
   int vmeta_n = 0, ncc_n = 0;  // FX: the next chunk's shifts and count
-  // compute-wave issue priority (PDD_CW_PRIO, tuning experiments): 1 =
-  // static by age (the youngest third highest), 2 = only the youngest third
-  // raised, 3 = rotating by chunk
-  auto cw_prio = [&](int k) {
-    const int a = (w * 3) / NCW;  // 0 oldest .. 2 youngest
-    int p = 0;
-    if constexpr (PDD_CW_PRIO == 1) p = a;
-    else if constexpr (PDD_CW_PRIO == 2) p = a == 2;
-    else if constexpr (PDD_CW_PRIO == 3) p = (a + k) % 3;
-    if constexpr (PDD_CW_PRIO != 0) {
-      if (p == 0) __builtin_amdgcn_s_setprio(0);
-      else if (p == 1) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(2);
-    }
-  };
-  cw_prio(0);
+  // (Measured and dropped, round 6: compute-wave issue priorities by age,
+  // raised for the youngest third, or rotating by chunk -- the older waves
+  // finish a chunk ~20% earlier and wait at its barrier, but the LDS stays
+  // saturated to the end of the chunk: configs[3] 89.5 ms per launch either
+  // way, DESIGN.md appendix.)
   __builtin_amdgcn_s_barrier();  // prologue barrier (metadata landed)
   asm volatile("" ::: "memory");
   if (stamps) tB = __builtin_amdgcn_s_memtime();
@@ -1471,7 +1457,6 @@ __global__ __launch_bounds__((NCW + NLW) * 64) void k_sweep_il(
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if constexpr (PDD_CW_PRIO == 3) cw_prio(k);
     if (stamps) { tB = __builtin_amdgcn_s_memtime(); ts_poll += tB - tA; }
     const int slot = k % MR;
     // ONE ds_read_b32 brings the wave's DPW shifts of all CC channels of the

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Tuning build of the working tree's production libpdd with extra defines
-# (PDD_FX_GT, PDD_CW_PRIO, ...) into build/libpdd_<name>.so, loaded with
+# (PDD_FX_GT, PDD_FX_PAIR_MAX, ...) into build/libpdd_<name>.so, loaded with
 # PDD_DEV_LIB=build/libpdd_<name>.so:  scripts/build_variant.sh <name> [-DFOO=1 ...]
 # (developer knobs -- stamps, timing-only decompositions: scripts/build_dev.sh)
 set -e

@@ -74,3 +74,38 @@ def test_pipeline_ordering_with_delayed_loopback_gather(gpu, rank):
         assert torch.equal(ds.plane(), plane[ds.lo:ds.hi]), "step %d" % step
     assert calls == list(range(NB)) * 2
     ds.close()
+
+
+@pytest.mark.parametrize("world,rank", [(1, 0), (4, 1), (4, 3)])
+def test_timeshard_host_step_device_equals_resident(gpu, world, rank):
+    """TimeShardedSweep.host_step on the device (the PCIe-inclusive leg of
+    bench.py at N > 1): the rank's input spectra in PINNED host memory, 4
+    H2D chunks on a copy stream (edges rounded up to 16 spectra) under 4
+    column ranges of the factorised 8-bit sweep -- the rank's plane equals
+    the resident step (__call__) bit for bit, and (W = 1) the one-shot
+    DMSweep plane."""
+    import torch
+    from pypulsar_amd.sharding import TimeShardedSweep
+    from pypulsar_amd.sweep import DMSweep
+    C, N, D = 1024, 1 << 18, 512
+    freqs = band(C)
+    dms = np.linspace(0.0, 1000.0, D)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(91)
+    block = torch.randint(0, 256, (N, C), generator=g, device="cuda", dtype=torch.uint8)
+    ts = TimeShardedSweep(dms, freqs, DT, N, dtype=torch.uint8, world=world, rank=rank,
+                          device="cuda")
+    assert ts.sw.factor_info(1)[0] in (2, 4)
+    lo, hi = ts.input_range()
+    want = ts(block[lo:hi].contiguous()).clone()
+    hpart = torch.empty((hi - lo, C), dtype=torch.uint8, pin_memory=True)
+    hpart.copy_(block[lo:hi])
+    ts.out.fill_(-1.0)
+    got = ts.host_step(hpart, n_batches=4)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
+    if world == 1:
+        sw = DMSweep(dms, freqs, DT, dtype="u8")
+        assert torch.equal(want, sw(block.t().contiguous()))
+        sw.close()
+    ts.close()
