@@ -1671,6 +1671,10 @@ static const Variant kF32Variants[] = {
 #define PDD_FX_DPW 8
 #endif
 static const Variant kU8FxVariants[] = {{0, false, 8, 2, PDD_FX_DPW, 12, 8, 2, 4}};
+// 8-bit input, short grids (plan_create): u16 eighths, DB 40 (10 compute +
+// 4 loader waves), reported as variant kShortVi
+static const Variant kU8Short = {0, false, 8, 2, 4, 10, 8, 2, 4};
+static constexpr int kShortVi = 100;
 static const Variant kU8Variants[] = {
     {0, false, 8, 2, 6, 12, 8, 2, 4},   // u16 eighths, DB 72: 6 trials per compute wave in the
                                         //   registers 4 took with float totals (k_sweep_il's
@@ -1705,6 +1709,8 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false) {
       return k_sweep_il<4, 4, 14, 2, 8, 2, false, true>;
     return nullptr;
   }
+  if (v.S == 8 && v.NW == 10 && v.NLW == 4 && v.G == 2 && v.CC == 8 && v.NBUF == 2 && v.DPW == 4)
+    return k_sweep_il<2, 4, 10, 4, 8, 2, true>;
   if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.CC == 8 && v.NBUF == 2) {
     if (v.DPW == 6) return k_sweep_il<2, 6, 12, 4, 8, 2, true>;
     if (v.DPW == 4) return k_sweep_il<2, 4, 12, 4, 8, 2, true>;
@@ -2590,11 +2596,19 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
   // 48-trial tiling when it pads the grid to >= 3% fewer trial slots
   // (configs[2] stage 1: 40 trials in 48 slots instead of 72)
   int v0 = 0;
-  if (int_in && cdiv(D, (int64_t)kU8Variants[1].DB()) * kU8Variants[1].DB() * 103 <
-                    cdiv(D, (int64_t)kU8Variants[0].DB()) * kU8Variants[0].DB() * 100)
-    v0 = 1;
-  for (int vi = (fv >= 0 && fv < ncand) ? fv : v0; vi < ncand; ++vi) {
-    const Variant v = cands[vi];
+  auto slots = [&](const Variant& x) { return cdiv(D, (int64_t)x.DB()) * x.DB(); };
+  if (int_in && slots(kU8Variants[1]) * 103 < slots(kU8Variants[0]) * 100) v0 = 1;
+  // ... and at the 40-trial tiling (kU8Short, reported as variant kShortVi)
+  // when that pads to >= 3% fewer slots again (configs[2] stage 1: 40 trials
+  // in 40 slots)
+  const bool short_first = int_in && fv < 0 &&
+                           slots(kU8Short) * 103 < std::min(slots(kU8Variants[0]), slots(kU8Variants[1])) * 100;
+  std::vector<std::pair<Variant, int>> cl;  // (tiling, its reported index)
+  if (short_first) cl.push_back({kU8Short, kShortVi});
+  for (int vi = (fv >= 0 && fv < ncand) ? fv : v0; vi < ncand; ++vi) cl.push_back({cands[vi], vi});
+  for (const auto& cv : cl) {
+    const Variant v = cv.first;
+    const int vi = cv.second;
     const bool il = v.kind == 0;
     if (n_grp > 1 && !il) continue;  // only the interleaved kernel sweeps groups
     if (dtype == PDD_U16 && !il) {     // the generic kernel reads 8-bit or float32 rows
