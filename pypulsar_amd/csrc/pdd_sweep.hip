@@ -1674,6 +1674,9 @@ static const Variant kU8FxVariants[] = {{0, false, 8, 2, PDD_FX_DPW, 12, 8, 2, 4
 // 8-bit input, short grids (plan_create): u16 eighths, DB 40 (10 compute +
 // 4 loader waves), reported as variant kShortVi
 static const Variant kU8Short = {0, false, 8, 2, 4, 10, 8, 2, 4};
+// float32 input, grouped short grids: quarters, DB 52 (13 compute + 3 loader
+// waves; configs[2] stage 2: 50 trials per pass in 52 slots instead of 56)
+static const Variant kF32Short = {0, false, 4, 4, 4, 13, 8, 2, 3};
 static constexpr int kShortVi = 100;
 static const Variant kU8Variants[] = {
     {0, false, 8, 2, 6, 12, 8, 2, 4},   // u16 eighths, DB 72: 6 trials per compute wave in the
@@ -1716,6 +1719,7 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false) {
     if (v.DPW == 4) return k_sweep_il<2, 4, 12, 4, 8, 2, true>;
   }
   if (v.S == 4 && v.G == 4 && v.DPW == 4 && v.CC == 8 && v.NBUF == 2) {
+    if (v.NW == 13 && v.NLW == 3) return k_sweep_il<4, 4, 13, 3, 8, 2>;
     if (v.NW == 14 && v.NLW == 2) return k_sweep_il<4, 4, 14, 2, 8, 2>;
     if (v.NW == 8 && v.NLW == 2) return k_sweep_il<4, 4, 8, 2, 8, 2>;
   }
@@ -2601,10 +2605,11 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
   // ... and at the 40-trial tiling (kU8Short, reported as variant kShortVi)
   // when that pads to >= 3% fewer slots again (configs[2] stage 1: 40 trials
   // in 40 slots)
-  const bool short_first = int_in && fv < 0 &&
-                           slots(kU8Short) * 103 < std::min(slots(kU8Variants[0]), slots(kU8Variants[1])) * 100;
+  const bool short_first =
+      fv < 0 && (int_in ? slots(kU8Short) * 103 < std::min(slots(kU8Variants[0]), slots(kU8Variants[1])) * 100
+                        : n_grp > 1 && slots(kF32Short) * 103 < slots(kF32Variants[0]) * 100);
   std::vector<std::pair<Variant, int>> cl;  // (tiling, its reported index)
-  if (short_first) cl.push_back({kU8Short, kShortVi});
+  if (short_first) cl.push_back({int_in ? kU8Short : kF32Short, kShortVi});
   for (int vi = (fv >= 0 && fv < ncand) ? fv : v0; vi < ncand; ++vi) cl.push_back({cands[vi], vi});
   for (const auto& cv : cl) {
     const Variant v = cv.first;
