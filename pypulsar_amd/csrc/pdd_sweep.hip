@@ -2602,12 +2602,15 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
   int v0 = 0;
   auto slots = [&](const Variant& x) { return cdiv(D, (int64_t)x.DB()) * x.DB(); };
   if (int_in && slots(kU8Variants[1]) * 103 < slots(kU8Variants[0]) * 100) v0 = 1;
-  // ... and at the 40-trial tiling (kU8Short, reported as variant kShortVi)
-  // when that pads to >= 3% fewer slots again (configs[2] stage 1: 40 trials
-  // in 40 slots)
+  // ... and grouped plans at the 40-trial tiling (kU8Short, reported as
+  // variant kShortVi) when that pads to >= 3% fewer slots again (configs[2]
+  // stage 1: 40 trials in 40 slots)
+  // (grouped plans only: single-group plans keep the tilings their
+  // factorised sweeps are instanced for)
   const bool short_first =
-      fv < 0 && (int_in ? slots(kU8Short) * 103 < std::min(slots(kU8Variants[0]), slots(kU8Variants[1])) * 100
-                        : n_grp > 1 && slots(kF32Short) * 103 < slots(kF32Variants[0]) * 100);
+      fv < 0 && n_grp > 1 &&
+      (int_in ? slots(kU8Short) * 103 < std::min(slots(kU8Variants[0]), slots(kU8Variants[1])) * 100
+              : slots(kF32Short) * 103 < slots(kF32Variants[0]) * 100);
   std::vector<std::pair<Variant, int>> cl;  // (tiling, its reported index)
   if (short_first) cl.push_back({int_in ? kU8Short : kF32Short, kShortVi});
   for (int vi = (fv >= 0 && fv < ncand) ? fv : v0; vi < ncand; ++vi) cl.push_back({cands[vi], vi});

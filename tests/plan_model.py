@@ -27,15 +27,13 @@ def choose(table, dtype):
     span."""
     cands = U8 if dtype == "u8" else F32
     D, C = table.shape
-    # short grids start at the 48-trial u16 tiling, or at the 40-trial one
-    # (reported as variant 100) when that pads less again (pdd_sweep.hip
-    # plan_create)
+    # short grids start at the 48-trial u16 tiling (pdd_sweep.hip
+    # plan_create; grouped plans may take a 40-trial one, variant 100)
     v0 = 0
     slots = lambda db: -(-D // db) * db
     if dtype == "u8" and slots(48) * 103 < slots(72) * 100:
         v0 = 1
-    if dtype == "u8" and slots(40) * 103 < min(slots(72), slots(48)) * 100:
-        return 100
+    # (grouped plans only; this model covers single-group plans)
     for vi, (kind, u8, S, G, DPW, NW, CC, NBUF, NLW) in enumerate(cands):
         if vi < v0:
             continue
