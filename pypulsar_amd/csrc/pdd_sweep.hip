@@ -2083,8 +2083,8 @@ struct FxTables {
 // group g at b[d][g] - sig[d].  With sig[d] = b[d][gr] - min over the block
 // (gr: a reference group near the middle of the band, the one minimising the
 // summed drift of b - sig over the groups) the drift of group g becomes
-// |drift(g) - drift(gr)|: the north star stages 27% fewer window elements,
-// configs[3] 21% (tests/plan_model.py).  The plane is the same
+// |drift(g) - drift(gr)|: the north star stages 24% fewer window elements,
+// configs[3] 19% (scripts/probes/fx_model.cpp).  The plane is the same
 // sum at the same (trial, column): only which tile produces a column changes
 // (each segment gets ceil(max sig / Tq) more time tiles; the kernel stores
 // elements inside [0, Qs) only).
