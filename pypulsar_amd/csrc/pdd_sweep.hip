@@ -1671,9 +1671,14 @@ static const Variant kF32Variants[] = {
 #define PDD_FX_DPW 8
 #endif
 static const Variant kU8FxVariants[] = {{0, false, 8, 2, PDD_FX_DPW, 12, 8, 2, 4}};
-// 8-bit input, short grids (plan_create): u16 eighths, DB 40 (10 compute +
-// 4 loader waves), reported as variant kShortVi
-static const Variant kU8Short = {0, false, 8, 2, 4, 10, 8, 2, 4};
+// 8-bit input, short grids (plan_create): u16 eighths, DB 40 in 8-wave
+// tiles (5 compute waves of 8 trials + 3 loaders, <= 78 KB of LDS, 120
+// VGPRs): two tiles per CU, so one tile's first window DMAs and plane stores
+// run under the other's reads.  Reported as variant kShortVi.  (configs[2]
+// stage-1 sweep 1.34 -> 1.12 ms against 10 + 4 waves, one tile per CU;
+// float32 short grids in 7 + 1-wave DB-28 tiles, two per CU: 1.60 -> 1.57
+// ms, not kept: each of the two trial blocks stages every window again.)
+static const Variant kU8Short = {0, false, 8, 2, 8, 5, 8, 2, 3};
 // float32 input, grouped short grids: quarters, DB 52 (13 compute + 3 loader
 // waves; configs[2] stage 2: 50 trials per pass in 52 slots instead of 56)
 static const Variant kF32Short = {0, false, 4, 4, 4, 13, 8, 2, 3};
@@ -1712,8 +1717,8 @@ static sweep_il_fn il_kernel_for(const Variant& v, bool fx = false) {
       return k_sweep_il<4, 4, 14, 2, 8, 2, false, true>;
     return nullptr;
   }
-  if (v.S == 8 && v.NW == 10 && v.NLW == 4 && v.G == 2 && v.CC == 8 && v.NBUF == 2 && v.DPW == 4)
-    return k_sweep_il<2, 4, 10, 4, 8, 2, true>;
+  if (v.S == 8 && v.NW == 5 && v.NLW == 3 && v.G == 2 && v.CC == 8 && v.NBUF == 2 && v.DPW == 8)
+    return k_sweep_il<2, 8, 5, 3, 8, 2, true>;
   if (v.S == 8 && v.NW == 12 && v.NLW == 4 && v.G == 2 && v.CC == 8 && v.NBUF == 2) {
     if (v.DPW == 6) return k_sweep_il<2, 6, 12, 4, 8, 2, true>;
     if (v.DPW == 4) return k_sweep_il<2, 4, 12, 4, 8, 2, true>;
@@ -2606,10 +2611,12 @@ static int plan_create(const int32_t* host_table, int64_t n_grp, int64_t D, int6
   // variant kShortVi) when that pads to >= 3% fewer slots again (configs[2]
   // stage 1: 40 trials in 40 slots)
   // (grouped plans only: single-group plans keep the tilings their
-  // factorised sweeps are instanced for)
+  // factorised sweeps are instanced for; kU8Short's 8 trials per wave keep
+  // byte-wide carry counts: plane sums <= 255 * 2^15)
   const bool short_first =
       fv < 0 && n_grp > 1 &&
-      (int_in ? slots(kU8Short) * 103 < std::min(slots(kU8Variants[0]), slots(kU8Variants[1])) * 100
+      (int_in ? slots(kU8Short) * 103 < std::min(slots(kU8Variants[0]), slots(kU8Variants[1])) * 100 &&
+                    C * (dtype == PDD_U8 ? 255 : 1023) <= 255 * 32768
               : slots(kF32Short) * 103 < slots(kF32Variants[0]) * 100);
   std::vector<std::pair<Variant, int>> cl;  // (tiling, its reported index)
   if (short_first) cl.push_back({int_in ? kU8Short : kF32Short, kShortVi});

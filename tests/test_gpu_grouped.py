@@ -254,3 +254,52 @@ def test_subband_chain_equals_stages(gpu, ds, padval):
     np.testing.assert_array_equal(got[6 + 2], want[:n_out])
     g1.close()
     g2.close()
+
+
+@pytest.mark.parametrize("case", ["u8_const255", "u16_const1023", "u8_extremes"])
+def test_grouped_short_tiling_saturated(gpu, case):
+    """Grouped short grids (40 trials per group) take the 8-wave DB-40 tiling
+    (variant 100: 8 trials per compute wave, byte-wide carry counts) up to the
+    plan's bound C x input <= 255 * 2^15.  const: every plane value equals
+    C x v; extremes (random 0 / 255): each group's rows equal the
+    single-group DMSweep over its channels (the 48-trial tiling, u16 carry
+    words).  Above the bound the plan falls back to the 48-trial tiling."""
+    import torch
+    from pypulsar_amd import _lib
+    from pypulsar_amd.sweep import DMSweep, GroupedSweep
+    N, D, G = 4096, 40, 2
+    if case == "u16_const1023":
+        C, dtype, v = 8167, "u16", 1023
+    else:
+        C, dtype, v = 32768, "u8", 255
+    freqs = band(C)
+    dms = np.linspace(0.0, 2.0, D)
+    sw = DMSweep(dms, freqs, DT, dtype=dtype, factor=False)
+    gs = GroupedSweep(np.stack([sw.table] * G), dtype)
+    assert gs.info()["variant"] == 100, gs.info()
+    if case == "u8_extremes":
+        g = torch.Generator(device="cuda")
+        g.manual_seed(11)
+        x = torch.randint(0, 2, (G * C, N), generator=g, device="cuda", dtype=torch.uint8) * 255
+    else:
+        x = torch.full((G * C, N), v, device="cuda",
+                       dtype=torch.uint8 if dtype == "u8" else torch.int16)
+    n_out = sw.n_out(N, True)
+    out = torch.full((G * D, n_out), -1.0, device="cuda")
+    pv = torch.full((G * C,), float(v), device="cuda")
+    gs(x, n_out, out, row_g=1, row_d=G, pad_mode=_lib.PAD_VALUE, padvals=pv)
+    if case == "u8_extremes":
+        for k in range(G):
+            want = sw(x[k * C:(k + 1) * C])
+            assert torch.equal(out[k::G], want), k
+    else:
+        assert 255 * 32768 - 1023 <= v * C <= 255 * 32768
+        assert torch.all(out == float(v * C)), (out.min().item(), out.max().item())
+    # one channel more than the bound: not the byte-carry tiling
+    big = GroupedSweep(np.stack([np.concatenate([sw.table, sw.table[:, :1]], 1)] * G)
+                       if v * (C + 1) > 255 * 32768 else np.stack([sw.table] * G), dtype)
+    if v * (C + 1) > 255 * 32768:
+        assert big.info()["variant"] != 100, big.info()
+    big.close()
+    gs.close()
+    sw.close()
