@@ -43,8 +43,10 @@ constexpr int kSpStarts = kSpWin * kSpWpb;         // 4096 starts per block
 constexpr int kSpSpan = kSpStarts + kSpMaxHalo;    // 5120 z values
 constexpr int kSpPer = kSpSpan / kSpThreads;       // 20 per thread (scan)
 constexpr int kSpR = kSpStarts / kSpThreads;       // 16 starts per thread
+constexpr int kSpStat = 64;                        // chunk statistics staged per block
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct Widths {
   int n;
@@ -70,21 +72,45 @@ __global__ __launch_bounds__(256) void k_sp_stats(const float* __restrict__ x, i
   const int len = (int)((t0 + L <= n) ? L : n - t0);
   const float* row = x + d * ld + t0;
   const float K = row[0];
+  // lane l sums samples 4 (l + 64 i) + e in (i, e) order, by 16-byte loads
+  // where the chunk start is 16-byte aligned and its length a multiple of 4,
+  // by single loads otherwise: the same float sums either way (a streamed
+  // plane's chunks land at other alignments than the one-shot plane's).
+  // Loads past the chunk re-read its last group / sample (in bounds) and add
+  // K (i.e. 0), so each pass issues its loads before any use.
   float s1 = 0.f, s2 = 0.f;
-  int i = lane;
-#pragma unroll 4
-  for (; i + 192 < len; i += 256) {
-    const float a = __builtin_nontemporal_load(row + i) - K;
-    const float b = __builtin_nontemporal_load(row + i + 64) - K;
-    const float c = __builtin_nontemporal_load(row + i + 128) - K;
-    const float e = __builtin_nontemporal_load(row + i + 192) - K;
-    s1 += (a + b) + (c + e);
-    s2 += (a * a + b * b) + (c * c + e * e);
-  }
-  for (; i < len; i += 64) {
-    const float a = row[i] - K;
-    s1 += a;
-    s2 += a * a;
+  auto add = [&](const float (&a)[4][4], int i0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float c = (4 * (lane + 64 * (i0 + u)) + e < len) ? a[u][e] - K : 0.f;
+        s1 += c;
+        s2 += c * c;
+      }
+  };
+  if (((uintptr_t)row & 15) == 0 && (len & 3) == 0) {
+    for (int i0 = 0; 256 * i0 < len; i0 += 4) {
+      float a[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int b = 4 * (lane + 64 * (i0 + u));
+        const f32x4 q =
+            __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row + min(b, len - 4)));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[u][e] = q[e];
+      }
+      add(a, i0);
+    }
+  } else {
+    for (int i0 = 0; 256 * i0 < len; i0 += 4) {
+      float a[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[u][e] = row[min(4 * (lane + 64 * (i0 + u)) + e, len - 1)];
+      add(a, i0);
+    }
   }
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -99,8 +125,10 @@ __global__ __launch_bounds__(256) void k_sp_stats(const float* __restrict__ x, i
   }
 }
 
-// P[i] (LDS) is the exclusive prefix sum of z over the block's starts + halo,
-// relative to the block start, so snr(i, w) = (P[i + w] - P[i]) / sqrt(w).
+// P[zoff + i] (LDS) is the exclusive prefix sum of z over the block's starts
+// + halo, relative to the block start, so snr(i, w) = (P[zoff + i + w] -
+// P[zoff + i]) / sqrt(w); zoff = the row's misalignment on the 16-byte-load
+// path (z at P[zoff + i], zoff leading zeros), else 0.
 //   pass 1: per window, the maximum S/N over (width, start)  (sub, mul, max)
 //   pass 2: only for windows whose maximum reaches the threshold (rare): the
 //           first (width, start) in (width, start) order whose S/N -- the
@@ -112,13 +140,15 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_search(
     const float* __restrict__ mean_n, const float* __restrict__ istd_n, Widths W, float thr,
     int64_t nblk, int32_t* __restrict__ cands, int64_t max_cands,
     unsigned long long* __restrict__ count) {
-  __shared__ float P[kSpSpan + 1];
+  __shared__ __attribute__((aligned(16))) float P[kSpSpan + 4];
   __shared__ float wtot[kSpThreads / 64];
   __shared__ float wmax[kSpThreads / 64][kSpWpb];
   __shared__ int wkey[kSpThreads / 64][kSpWpb];
   __shared__ float bmax[kSpWpb];
+  __shared__ float smean[kSpStat], sistd[kSpStat];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t d = blockIdx.x / nblk, blk = blockIdx.x % nblk;
+  // (32-bit: D * nblk < 2^31, checked by the host)
+  const int64_t d = blockIdx.x / (uint32_t)nblk, blk = blockIdx.x % (uint32_t)nblk;
   const int64_t t0 = blk * kSpStarts;
   // the row is x[d][0:na] followed by xn[d][0:n-na] (a stream's next plane);
   // chunks k < nchunk use mean/istd, later ones mean_n/istd_n (na % L == 0)
@@ -132,9 +162,70 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_search(
   const int64_t nst = n - t0;  // start i is valid for width w when i + w <= nst
   const int64_t nss = n_starts - t0;  // ... and i < nss
 
-  // z of the starts + halo, coalesced, into P[1..]; the chunk index advances
-  // incrementally (one 64-bit division per thread, not per sample)
-  {
+  // z of the starts + halo, coalesced, into P[zoff..]: (x - mean_k) * istd_k
+  const int64_t k_lo = t0 / L, nks = (t0 + span - 1) / L - k_lo + 1;
+  // (16-byte loads need the block inside the first plane and, with the row's
+  // misalignment mis, the span plus mis inside the block's LDS span)
+  const int mis = (int)(((uintptr_t)(row + t0) >> 2) & 3);
+  const bool staged = L >= 4 && nks <= kSpStat && t0 + span <= na && span + mis <= kSpSpan;
+  const int zoff = staged ? mis : 0;  // where z[0] sits in P
+  if (staged) {
+    // the block's chunk statistics staged in LDS; thread tid loads the
+    // 16-byte-aligned groups 4 (tid + 256 j) of the row from mis elements
+    // before the block start (element i = 4 (tid + 256 j) + e - mis; a group
+    // past the last valid element re-reads that element's group, so every
+    // load stays in the 16-byte granules holding the row's own elements);
+    // every load is issued before the statistics are staged and used (at
+    // most one chunk boundary in 4 samples: L >= 4)
+    constexpr int NJ = kSpSpan / (4 * kSpThreads);
+    const float* rowA = row + t0 - mis;
+    const int amax = (mis + (int)span - 1) & ~3;
+    // (the statistics first: their LDS stores wait for them alone)
+    float sm = 0.f, si = 0.f;
+    if (tid < nks) {
+      const int64_t k = k_lo + tid;
+      sm = (k < nchunk ? mrow : mnrow)[k];
+      si = (k < nchunk ? irow : inrow)[k];
+    }
+    f32x4 q[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      q[j] = __builtin_nontemporal_load(
+          reinterpret_cast<const f32x4*>(rowA + min(4 * (tid + kSpThreads * j), amax)));
+    if (tid < nks) {
+      smean[tid] = sm;
+      sistd[tid] = si;
+    }
+    // (z lands at P[i + mis], 16-byte aligned, after mis zeros)
+    // chunk index of the thread's first element: 32-bit (t < 2^31; L
+    // clamped, which changes no quotient)
+    const uint32_t L32 = (uint32_t)min(L, (int64_t)0x7fffffff);
+    const int64_t k = (uint32_t)(t0 + max(4 * tid - mis, 0)) / L32;
+    // block-relative: chunk kr (of the staged ones) ends before element rb
+    int kr = (int)(k - k_lo);
+    int rb = (int)min((k + 1) * L - t0, (int64_t)0x7fffffff);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int i = 4 * (tid + kSpThreads * j) - mis;
+      while (i >= rb) {
+        ++kr;
+        rb = (int)min((int64_t)rb + L32, (int64_t)0x7fffffff);
+      }
+      // the group's chunk and, past rb, the next one
+      const int ka = min(kr, (int)nks - 1), kb = min(kr + 1, (int)nks - 1);
+      const float ma = smean[ka], ia = sistd[ka], mb = smean[kb], ib = sistd[kb];
+      f32x4 z;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool nx = i + e >= rb;
+        z[e] = (i + e >= 0 && i + e < span) ? (q[j][e] - (nx ? mb : ma)) * (nx ? ib : ia) : 0.f;
+      }
+      *reinterpret_cast<f32x4*>(P + i + mis) = z;
+    }
+  } else {
+    // (short chunks or a block over many: per sample, the chunk index
+    // advancing incrementally -- one 64-bit division per thread)
     int64_t k = (t0 + tid) / L, nb = (k + 1) * L;
     for (int i = tid; i < kSpSpan; i += kSpThreads) {
       float z = 0.f;
@@ -148,7 +239,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_search(
         const float v = __builtin_nontemporal_load((a ? row : nrow) + t);
         z = (v - (k < nchunk ? mrow : mnrow)[k]) * (k < nchunk ? irow : inrow)[k];
       }
-      P[i + 1] = z;
+      P[i] = z;
     }
   }
   __syncthreads();
@@ -157,7 +248,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_search(
   float loc = 0.f;
 #pragma unroll
   for (int j = 0; j < kSpPer; ++j) {
-    v[j] = P[1 + tid * kSpPer + j];
+    v[j] = P[tid * kSpPer + j];
     loc += v[j];
   }
   float inc = loc;
@@ -180,26 +271,34 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_search(
 
   // pass 1: per-window maxima; start i = tid + 256 r lies in window r / 4
   float p0[kSpR];
+  const float* Pz = P + zoff;
 #pragma unroll
-  for (int r = 0; r < kSpR; ++r) p0[r] = P[tid + kSpThreads * r];
+  for (int r = 0; r < kSpR; ++r) p0[r] = Pz[tid + kSpThreads * r];
   float m[kSpWpb];
 #pragma unroll
   for (int q = 0; q < kSpWpb; ++q) m[q] = -INFINITY;
   if (nst >= kSpStarts - 1 + W.maxw && nss >= kSpStarts) {
     // interior block: every (start, width) valid; starts in pairs through
-    // packed f32 (v_pk_add_f32 / v_pk_mul_f32), maxima through v_max3_f32
+    // packed f32 (v_pk_add_f32), maxima through v_max3_f32.  Per width the
+    // window's largest sum first, scaled once: rounding x -> x * (1/sqrt w)
+    // is monotonic, so max((a - b) * s) == max(a - b) * s bit for bit (and
+    // pass 2 finds the same float)
     for (int wi = 0; wi < W.n; ++wi) {
       const int w = W.w[wi];
-      const f32x2 iw = {W.inv_sqrt[wi], W.inv_sqrt[wi]};
+      float mw[kSpWpb];
+#pragma unroll
+      for (int q = 0; q < kSpWpb; ++q) mw[q] = -INFINITY;
 #pragma unroll
       for (int r = 0; r < kSpR; r += 2) {
         const int i = tid + kSpThreads * r;
-        const f32x2 a = {P[i + w], P[i + kSpThreads + w]};
+        const f32x2 a = {Pz[i + w], Pz[i + kSpThreads + w]};
         const f32x2 b = {p0[r], p0[r + 1]};
-        const f32x2 snr = (a - b) * iw;
+        const f32x2 sum = a - b;
         const int q = r / (kSpR / kSpWpb);
-        m[q] = fmaxf(fmaxf(m[q], snr.x), snr.y);
+        mw[q] = fmaxf(fmaxf(mw[q], sum.x), sum.y);
       }
+#pragma unroll
+      for (int q = 0; q < kSpWpb; ++q) m[q] = fmaxf(m[q], mw[q] * W.inv_sqrt[wi]);
     }
   } else {
     for (int wi = 0; wi < W.n; ++wi) {
@@ -208,7 +307,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_search(
 #pragma unroll
       for (int r = 0; r < kSpR; ++r) {
         const int i = tid + kSpThreads * r;
-        const float snr = (i + w <= nst && i < nss) ? (P[i + w] - p0[r]) * iw : -INFINITY;
+        const float snr = (i + w <= nst && i < nss) ? (Pz[i + w] - p0[r]) * iw : -INFINITY;
         m[r / (kSpR / kSpWpb)] = fmaxf(m[r / (kSpR / kSpWpb)], snr);
       }
     }
@@ -242,7 +341,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_search(
 #pragma unroll
     for (int r = 0; r < kSpR; ++r) {
       const int i = tid + kSpThreads * r, q = r / (kSpR / kSpWpb);
-      const float snr = (i + w <= nst && i < nss) ? (P[i + w] - p0[r]) * iw : -INFINITY;
+      const float snr = (i + w <= nst && i < nss) ? (Pz[i + w] - p0[r]) * iw : -INFINITY;
       if (bmax[q] >= thr && snr == bmax[q]) key[q] = min(key[q], wi * kSpStarts + i);
     }
   }
