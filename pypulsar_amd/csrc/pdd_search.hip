@@ -55,11 +55,30 @@ struct Widths {
   float inv_sqrt[kSpMaxWidths];
 };
 
+// Lane 0's value after an xor butterfly over the wave (the same association
+// as __shfl_xor steps 1, 2, ..., 32): steps 1..16 by ds_swizzle within each
+// 32-lane half (no address arithmetic), step 32 by two readlanes.
+template <int XOR>
+__device__ __forceinline__ float swz_xor(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v),
+                                                               0x1F | (XOR << 10)));
+}
+template <typename Op>
+__device__ __forceinline__ float wave_reduce0(float v, Op op) {
+  v = op(v, swz_xor<1>(v));
+  v = op(v, swz_xor<2>(v));
+  v = op(v, swz_xor<4>(v));
+  v = op(v, swz_xor<8>(v));
+  v = op(v, swz_xor<16>(v));
+  return op(__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0)),
+            __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32)));
+}
+
 // one wave per (row, chunk), 4 per block: the chunk is read once, coalesced,
 // as shifted sums S1 = sum(x - K), S2 = sum((x - K)^2) with K the chunk's
 // first sample, so var = S2/len - (S1/len)^2 does not cancel against a large
 // mean (plane rows sit at ~C x 128 for 8-bit input) and f32 is enough; both
-// sums go through one butterfly reduction (two independent chains).
+// sums go through one butterfly reduction (wave_reduce0).
 __global__ __launch_bounds__(256) void k_sp_stats(const float* __restrict__ x, int64_t D, int64_t n,
                                                   int64_t ld, int64_t L, int64_t nchunk,
                                                   float* __restrict__ mean_out,
@@ -112,11 +131,9 @@ __global__ __launch_bounds__(256) void k_sp_stats(const float* __restrict__ x, i
       add(a, i0);
     }
   }
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    s1 += __shfl_xor(s1, o, 64);
-    s2 += __shfl_xor(s2, o, 64);
-  }
+  const auto plus = [](float a, float b) { return a + b; };
+  s1 = wave_reduce0(s1, plus);
+  s2 = wave_reduce0(s2, plus);
   if (lane == 0) {
     const float m1 = s1 / (float)len;
     const float var = fmaxf(s2 / (float)len - m1 * m1, 0.f);
@@ -314,8 +331,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_search(
   }
 #pragma unroll
   for (int q = 0; q < kSpWpb; ++q) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m[q] = fmaxf(m[q], __shfl_xor(m[q], o, 64));
+    m[q] = wave_reduce0(m[q], [](float a, float b) { return fmaxf(a, b); });
     if (lane == 0) wmax[wv][q] = m[q];
   }
   __syncthreads();
