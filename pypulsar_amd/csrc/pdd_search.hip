@@ -17,7 +17,8 @@
 //      over the window's starts and all widths (ties: smallest width, then
 //      smallest start), kept when >= threshold.
 //
-// Kernels (both meant to be HBM-bound: each reads the plane once):
+// Kernels (each reads the plane once; k_sp_search is VALU-bound, DESIGN.md
+// §6b):
 //   k_sp_stats   one wave per chunk: single-pass shifted sums, one butterfly
 //   k_sp_search  one 256-thread block per (row, 4 windows of 1024 starts): z
 //                of the starts + halo (max width - 1) into LDS, block prefix
@@ -180,7 +181,10 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_search(
   const int64_t nss = n_starts - t0;  // ... and i < nss
 
   // z of the starts + halo, coalesced, into P[zoff..]: (x - mean_k) * istd_k
-  const int64_t k_lo = t0 / L, nks = (t0 + span - 1) / L - k_lo + 1;
+  // (32-bit quotients: t0 + span <= nt < 2^31, checked by the host; L
+  // clamped, which changes no quotient)
+  const uint32_t L32 = (uint32_t)min(L, (int64_t)0x7fffffff);
+  const int64_t k_lo = (uint32_t)t0 / L32, nks = (uint32_t)(t0 + span - 1) / L32 - k_lo + 1;
   // (16-byte loads need the block inside the first plane and, with the row's
   // misalignment mis, the span plus mis inside the block's LDS span)
   const int mis = (int)(((uintptr_t)(row + t0) >> 2) & 3);
@@ -214,9 +218,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_search(
       sistd[tid] = si;
     }
     // (z lands at P[i + mis], 16-byte aligned, after mis zeros)
-    // chunk index of the thread's first element: 32-bit (t < 2^31; L
-    // clamped, which changes no quotient)
-    const uint32_t L32 = (uint32_t)min(L, (int64_t)0x7fffffff);
+    // chunk index of the thread's first element
     const int64_t k = (uint32_t)(t0 + max(4 * tid - mis, 0)) / L32;
     // block-relative: chunk kr (of the staged ones) ends before element rb
     int kr = (int)(k - k_lo);
